@@ -1,0 +1,363 @@
+"""CPU oracle for PVNet's RANSAC-voting hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import this module, and only as the checker / the timed CPU baseline.
+The product package ``pvnet_amd`` never imports it.
+
+Two layers:
+
+* the kernel arithmetic (``generate_hypothesis``, ``voting_for_hypothesis``,
+  their vanishing-point twins and the mask-free ``vote_counts``) is plain C in
+  ``oracle/pvvote_oracle.c`` (IEEE fp32, no contraction), called via ctypes;
+* the control flow of the Python voting layer
+  ``lib/ransac_voting_gpu_layer/ransac_voting_gpu.py`` (cited ``RV:<line>``) is
+  restated below in numpy float32, step for step.
+
+Parity pinning: ``tests/golden/*.npz`` were produced by the reference's own
+``ransac_voting_gpu.py`` (see ``tests/golden/make_golden.py``); the oracle is
+tested against them in ``tests/test_oracle_golden.py``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+_f32p = ctypes.POINTER(ctypes.c_float)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+def build(force: bool = False) -> str:
+    """Compile liboracle.so with the committed Makefile (gcc only)."""
+    if force or not os.path.exists(_LIB_PATH) or \
+            os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "pvvote_oracle.c")):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.or_generate_hypothesis.argtypes = [_f32p, _f32p, _i32p, _f32p] + [ctypes.c_int] * 3
+        L.or_generate_hypothesis_vp.argtypes = L.or_generate_hypothesis.argtypes
+        L.or_voting_for_hypothesis.argtypes = [_f32p, _f32p, _f32p, _u8p] + [ctypes.c_int] * 3 + [ctypes.c_float]
+        L.or_voting_for_hypothesis_vp.argtypes = L.or_voting_for_hypothesis.argtypes
+        L.or_vote_counts.argtypes = [_f32p, _f32p, _f32p, _i64p] + [ctypes.c_int] * 3 + [ctypes.c_float, ctypes.c_int]
+        L.or_vote_test.argtypes = [ctypes.c_float] * 7
+        L.or_vote_test.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray, t):
+    return a.ctypes.data_as(t)
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+# ----------------------------------------------------------------------------
+# kernel arithmetic (ransac_voting_kernel.cu)
+# ----------------------------------------------------------------------------
+def generate_hypothesis(direct, coords, idxs):
+    """KU:11-86 -> f32 [hn,vn,2]; degenerate pairs stay 0 (KU:75)."""
+    direct, coords, idxs = _c(direct, np.float32), _c(coords, np.float32), _c(idxs, np.int32)
+    tn, vn = direct.shape[0], direct.shape[1]
+    hn = idxs.shape[0]
+    out = np.zeros((hn, vn, 2), np.float32)
+    lib().or_generate_hypothesis(_p(direct, _f32p), _p(coords, _f32p), _p(idxs, _i32p), _p(out, _f32p), tn, vn, hn)
+    return out
+
+
+def generate_hypothesis_vanishing_point(direct, coords, idxs):
+    """KU:170-266 -> f32 [hn,vn,3]."""
+    direct, coords, idxs = _c(direct, np.float32), _c(coords, np.float32), _c(idxs, np.int32)
+    tn, vn = direct.shape[0], direct.shape[1]
+    hn = idxs.shape[0]
+    out = np.zeros((hn, vn, 3), np.float32)
+    lib().or_generate_hypothesis_vp(_p(direct, _f32p), _p(coords, _f32p), _p(idxs, _i32p), _p(out, _f32p), tn, vn, hn)
+    return out
+
+
+def voting_for_hypothesis(direct, coords, hypo, inliers, inlier_thresh):
+    """KU:88-167, in place on a C-contiguous u8 [hn,vn,tn] array (ORs in 1s)."""
+    assert inliers.dtype == np.uint8 and inliers.flags["C_CONTIGUOUS"]
+    direct, coords, hypo = _c(direct, np.float32), _c(coords, np.float32), _c(hypo, np.float32)
+    tn, vn, hn = direct.shape[0], direct.shape[1], hypo.shape[0]
+    lib().or_voting_for_hypothesis(_p(direct, _f32p), _p(coords, _f32p), _p(hypo, _f32p), _p(inliers, _u8p),
+                                   tn, vn, hn, float(inlier_thresh))
+
+
+def voting_for_hypothesis_vanishing_point(direct, coords, hypo, inliers, inlier_thresh):
+    """KU:268-351, in place."""
+    assert inliers.dtype == np.uint8 and inliers.flags["C_CONTIGUOUS"]
+    direct, coords, hypo = _c(direct, np.float32), _c(coords, np.float32), _c(hypo, np.float32)
+    tn, vn, hn = direct.shape[0], direct.shape[1], hypo.shape[0]
+    lib().or_voting_for_hypothesis_vp(_p(direct, _f32p), _p(coords, _f32p), _p(hypo, _f32p), _p(inliers, _u8p),
+                                      tn, vn, hn, float(inlier_thresh))
+
+
+def vote_counts(direct, coords, hypo, inlier_thresh, nthreads=0):
+    """int64 [hn,vn] = torch.sum(inliers, 2) of a fresh vote (RV:563-567)."""
+    direct, coords, hypo = _c(direct, np.float32), _c(coords, np.float32), _c(hypo, np.float32)
+    tn, vn, hn = direct.shape[0], direct.shape[1], hypo.shape[0]
+    out = np.zeros((hn, vn), np.int64)
+    lib().or_vote_counts(_p(direct, _f32p), _p(coords, _f32p), _p(hypo, _f32p), _p(out, _i64p),
+                         tn, vn, hn, float(inlier_thresh), int(nthreads))
+    return out
+
+
+def vote_test(nx, ny, cx, cy, hx, hy, thr) -> int:
+    return int(lib().or_vote_test(nx, ny, cx, cy, hx, hy, thr))
+
+
+# ----------------------------------------------------------------------------
+# control flow (ransac_voting_gpu.py)
+# ----------------------------------------------------------------------------
+F32 = np.float32
+
+
+def fg_mask_v3(mask2d: np.ndarray) -> np.ndarray:
+    """RV:533 ``mask[bi].byte()``: truncate to uint8, non-zero = foreground."""
+    m = np.asarray(mask2d)
+    if m.dtype == np.bool_:
+        return m.copy()
+    return (m.astype(np.int64) & 0xFF) != 0
+
+
+def fg_mask_evd(mask2d: np.ndarray) -> np.ndarray:
+    """RV:340 / RV:273 ``mask[bi] == k + 1`` with k = 0."""
+    return np.asarray(mask2d) == 1
+
+
+def compact(fg: np.ndarray, vertex_hw: np.ndarray):
+    """RV:548-552: coords = nonzero(mask)[:, [1,0]] (x=col, y=row, row-major);
+    direct = vertex.masked_select(mask) -> [tn,vn,2]."""
+    rows, cols = np.nonzero(fg)
+    coords = np.stack([cols, rows], 1).astype(F32)
+    direct = np.ascontiguousarray(vertex_hw[rows, cols], dtype=F32)
+    return coords, direct
+
+
+def downsample(fg: np.ndarray, max_num: int, rng: np.random.Generator, keep: np.ndarray | None = None):
+    """RV:543-546: Bernoulli(max_num/fg) keep-mask.  The reference draws it from
+    the device RNG, which cannot be reproduced; tests inject ``keep``."""
+    if keep is None:
+        sel = rng.random(fg.shape, dtype=F32)
+        keep = sel < F32(F32(max_num) / F32(fg.sum()))
+    return fg & keep
+
+
+def argmax_first(x: np.ndarray, axis: int):
+    """torch.max(x, dim) index: first occurrence of the max."""
+    return np.argmax(x, axis=axis)
+
+
+def lu2_solve_inv(A: np.ndarray):
+    """Inverse of one f32 2x2 matrix the way LAPACK sgesv(A, I) computes it
+    (partial pivoting, first max on ties); None if a pivot is exactly zero,
+    which is when torch.gesv raises (RV:514)."""
+    a00, a01, a10, a11 = (F32(v) for v in (A[0, 0], A[0, 1], A[1, 0], A[1, 1]))
+    perm = (0, 1)
+    if abs(a10) > abs(a00):
+        a00, a01, a10, a11 = a10, a11, a00, a01
+        perm = (1, 0)
+    if a00 == 0:
+        return None
+    l = F32(a10 / a00)
+    u11 = F32(a11 - F32(l * a01))
+    if u11 == 0:
+        return None
+    inv = np.zeros((2, 2), F32)
+    for j in range(2):
+        e = np.zeros(2, F32)
+        e[j] = 1
+        bj = e[list(perm)]
+        y0 = bj[0]
+        y1 = F32(bj[1] - F32(l * y0))
+        x1 = F32(y1 / u11)
+        x0 = F32(F32(y0 - F32(a01 * x1)) / a00)
+        inv[0, j], inv[1, j] = x0, x1
+    return inv
+
+
+def b_inv(b_mat: np.ndarray) -> np.ndarray:
+    """RV:503-518 with torch.gesv available (the pinned torch 1.1/1.4):
+    batched inverse, and the IDENTITY for the whole batch as soon as one
+    matrix is singular (the bare ``except``)."""
+    out = np.empty_like(b_mat, dtype=F32)
+    for i in range(b_mat.shape[0]):
+        inv = lu2_solve_inv(b_mat[i])
+        if inv is None:
+            return np.broadcast_to(np.eye(2, dtype=F32), b_mat.shape).copy()
+        out[i] = inv
+    return out
+
+
+def stop_iterations(win_ratio_min: float, hn: int, confidence: float, max_iter: int) -> int:
+    """RV:578-582.  idxs are drawn once (RV:553), so every iteration re-creates
+    the same hypotheses and the best state never changes after iteration 1;
+    the loop length only decides how often that identical work repeats."""
+    r = F32(win_ratio_min)
+    hyp_num, it = 0, 0
+    while True:
+        hyp_num += hn
+        it += 1
+        val = F32(1) - np.power(F32(1) - r * r, F32(hyp_num), dtype=F32)
+        if val > confidence or it > max_iter:
+            return it
+
+
+def refine(direct, coords, win_pts, inlier_thresh):
+    """RV:584-601: least squares over the winner's inliers -> [vn,2]."""
+    tn, vn = direct.shape[0], direct.shape[1]
+    inl = np.zeros((1, vn, tn), np.uint8)
+    voting_for_hypothesis(direct, coords, win_pts[None], inl, inlier_thresh)
+    normal = np.zeros_like(direct)
+    normal[:, :, 0] = direct[:, :, 1]
+    normal[:, :, 1] = -direct[:, :, 0]
+    inl = inl[0].astype(F32)                                   # [vn,tn]
+    normal = normal.transpose(1, 0, 2) * inl[:, :, None]       # [vn,tn,2]
+    bb = (normal * coords[None]).sum(2, dtype=F32)             # [vn,tn] (2-term fp32 sums, exact order)
+    # RV:598-599 sum ~tn fp32 terms in torch's (unspecified) order; the oracle
+    # accumulates in float64 and rounds once, i.e. the correctly rounded sum.
+    n64 = normal.astype(np.float64)
+    ATA = np.matmul(n64.transpose(0, 2, 1), n64).astype(F32)               # [vn,2,2]
+    ATb = (n64 * bb.astype(np.float64)[:, :, None]).sum(1).astype(F32)     # [vn,2]
+    pts = np.matmul(b_inv(ATA), ATb[:, :, None])               # [vn,2,1]
+    return pts[:, :, 0].astype(F32), ATA, ATb
+
+
+def ransac_voting_layer_v3(mask, vertex, round_hyp_num, inlier_thresh=0.99, confidence=0.99, max_iter=100,
+                           min_num=100, max_num=30000, idxs=None, keep=None, seed=0, diag=None):
+    """RV:520-604.  ``mask`` [b,h,w], ``vertex`` [b,h,w,vn,2] (numpy).
+    ``idxs[bi]`` injects the hypothesis pixel pairs that the reference draws
+    with ``random_`` (RV:553); ``keep[bi]`` the downsampling mask (RV:543)."""
+    mask, vertex = np.asarray(mask), np.asarray(vertex, dtype=F32)
+    b, h, w, vn, _ = vertex.shape
+    rng = np.random.default_rng(seed)
+    out = np.zeros((b, vn, 2), F32)
+    for bi in range(b):
+        d = {}
+        fg = fg_mask_v3(mask[bi])
+        fgn = int(fg.sum())
+        d["foreground"] = fgn
+        if fgn < min_num:                                       # RV:537-540
+            d["skipped"] = True
+            if diag is not None:
+                diag.append(d)
+            continue
+        if fgn > max_num:                                       # RV:543-546
+            fg = downsample(fg, max_num, rng, None if keep is None else keep[bi])
+        coords, direct = compact(fg, vertex[bi])
+        tn = coords.shape[0]
+        cur_idxs = rng.integers(0, tn, size=(round_hyp_num, vn, 2), dtype=np.int32) if idxs is None \
+            else np.asarray(idxs[bi], np.int32)
+        hyp = generate_hypothesis(direct, coords, cur_idxs)
+        counts = vote_counts(direct, coords, hyp, inlier_thresh)
+        win_idx = argmax_first(counts, 0)                       # RV:568
+        win_counts = counts[win_idx, np.arange(vn)]
+        win_ratio = win_counts.astype(F32) / F32(tn)            # RV:570
+        all_ratio = np.zeros(vn, F32)
+        all_pts = np.zeros((vn, 2), F32)
+        larger = all_ratio < win_ratio                          # RV:573-575
+        all_pts[larger] = hyp[win_idx, np.arange(vn)][larger]
+        all_ratio[larger] = win_ratio[larger]
+        iters = stop_iterations(all_ratio.min(), round_hyp_num, confidence, max_iter)
+        pts, ATA, ATb = refine(direct, coords, all_pts, inlier_thresh)
+        out[bi] = pts
+        d.update(tn=tn, idxs=cur_idxs, hyp=hyp, counts=counts, win_idx=win_idx, win_ratio=all_ratio,
+                 win_pts=all_pts, iters=iters, ATA=ATA, ATb=ATb, coords=coords, direct=direct)
+        if diag is not None:
+            diag.append(d)
+    return out
+
+
+def _evd_collect(mask, vertex, round_hyp_num, min_hyp_num, inlier_thresh, min_num, max_num,
+                 idxs, keep, seed, guard_hyp_num):
+    mask, vertex = np.asarray(mask), np.asarray(vertex, dtype=F32)
+    b, h, w, vn, _ = vertex.shape
+    rng = np.random.default_rng(seed)
+    all_hyp, all_ratio = [], []
+    rounds = int(np.ceil(min_hyp_num / round_hyp_num))
+    for bi in range(b):
+        fg = fg_mask_evd(mask[bi])
+        fgn = int(fg.sum())
+        if fgn < min_num:                                       # RV:343-348 / RV:276-281
+            all_hyp.append(np.zeros((guard_hyp_num, vn, 2), F32))
+            all_ratio.append(np.ones((guard_hyp_num, vn), F32))
+            continue
+        if fgn > max_num:                                       # RV:351-355: foreground re-counted
+            fg = downsample(fg, max_num, rng, None if keep is None else keep[bi])
+            fgn = int(fg.sum())
+        coords, direct = compact(fg, vertex[bi])
+        tn = coords.shape[0]
+        hyps, ratios = [], []
+        for r in range(rounds):                                 # RV:365-379
+            cur = rng.integers(0, tn, size=(round_hyp_num, vn, 2), dtype=np.int32) if idxs is None \
+                else np.asarray(idxs[bi][r], np.int32)
+            hyp = generate_hypothesis(direct, coords, cur)
+            cnt = vote_counts(direct, coords, hyp, inlier_thresh)
+            hyps.append(hyp)
+            ratios.append(cnt.astype(F32) / F32(fgn))
+        all_hyp.append(np.concatenate(hyps, 0))
+        all_ratio.append(np.concatenate(ratios, 0))
+    hyp = np.stack(all_hyp, 0).transpose(0, 2, 1, 3)            # b,vn,hn,2
+    ratio = np.stack(all_ratio, 0).transpose(0, 2, 1).copy()    # b,vn,hn
+    return hyp, ratio
+
+
+def estimate_voting_distribution_with_mean(mask, vertex, mean, round_hyp_num=256, min_hyp_num=4096, topk=128,
+                                           inlier_thresh=0.99, min_num=20, max_num=30000, output_hyp=False,
+                                           idxs=None, keep=None, seed=0):
+    """RV:333-406 -> (mean, cov [b,vn,2,2])."""
+    hyp, ratio = _evd_collect(mask, vertex, round_hyp_num, min_hyp_num, inlier_thresh, min_num, max_num,
+                              idxs, keep, seed, guard_hyp_num=min_hyp_num)
+    mean = np.asarray(mean, F32)
+    thresh = ratio.max(2) - F32(0.1)                            # RV:394
+    ratio[ratio < thresh[:, :, None]] = 0                       # RV:395
+    diff = hyp - mean[:, :, None]                               # RV:398
+    wdiff = diff * ratio[..., None]
+    cov = np.matmul(diff.transpose(0, 1, 3, 2), wdiff)          # RV:400
+    cov = cov / (ratio.sum(2, dtype=F32)[:, :, None, None] + F32(1e-3))   # RV:401
+    return mean, cov.astype(F32)
+
+
+def topk_scatter(ratio: np.ndarray, topk: int) -> np.ndarray:
+    """RV:320-321 ``topk(sorted=False)`` + scatter into zeros.  Ties at the
+    k-th value are resolved lowest-index-first (torch leaves them unspecified)."""
+    out = np.zeros_like(ratio)
+    order = np.argsort(-ratio, axis=-1, kind="stable")[..., :topk]
+    np.put_along_axis(out, order, np.take_along_axis(ratio, order, -1), -1)
+    return out
+
+
+def estimate_voting_distribution(mask, vertex, round_hyp_num=256, min_hyp_num=4096, topk=128,
+                                 inlier_thresh=0.99, min_num=5, max_num=30000, idxs=None, keep=None, seed=0):
+    """RV:263-331 -> (mean, cov)."""
+    hyp, ratio = _evd_collect(mask, vertex, round_hyp_num, min_hyp_num, inlier_thresh, min_num, max_num,
+                              idxs, keep, seed, guard_hyp_num=round_hyp_num)
+    ratio = topk_scatter(ratio, topk)
+    wsum = ratio.sum(2, dtype=F32)
+    mean = (ratio[..., None] * hyp).sum(2, dtype=F32) / wsum[:, :, None]      # RV:323-324
+    diff = hyp - mean[:, :, None]
+    wdiff = diff * ratio[..., None]
+    cov = np.matmul(diff.transpose(0, 1, 3, 2), wdiff) / wsum[:, :, None, None]  # RV:326-329
+    return mean.astype(F32), cov.astype(F32)
+
+
+def argmax_mask(seg_pred: np.ndarray) -> np.ndarray:
+    """torch.argmax(seg_pred, 1) (DEMO:52): first max wins; NaN counts as max."""
+    s = np.asarray(seg_pred)
+    return np.argmax(np.where(np.isnan(s), np.inf, s), axis=1).astype(np.int64)
