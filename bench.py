@@ -1,0 +1,316 @@
+"""Benchmark: images/sec of PVNet's vote -> keypoint hot path on MI355X.
+
+One step = one batch of synthetic 480x640, 9-keypoint fields (generator S(seed),
+~30k foreground pixels) already resident in HBM, pushed
+through ``ransac_voting_layer_v3`` in its fused network-layout form
+(seg_pred argmax + compaction + 512 hypotheses/keypoint + vote/count + LS
+refine), captured as a hipGraph.  Multi-GPU: one process per GPU, images
+sharded round-robin (weak scaling), one RCCL gather of the keypoints of the
+whole stream to rank 0 at the end of the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0 (contract in the task statement).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level table)
+HBM_PEAK_GBS = 8000.0
+FP32_VECTOR_PEAK_TFLOPS = 157.3
+H, W, VN = 480, 640, 9
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=1, help="images per GPU per step (configs[1]: batch=1)")
+    ap.add_argument("--hn", type=int, default=512, help="round_hyp_num (DEMO:55 / TRAIN:141)")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--skip-cpu", action="store_true")
+    ap.add_argument("--skip-e2e", action="store_true")
+    ap.add_argument("--skip-u1", action="store_true")
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return ws, rank, torch.device("cuda", local if ws > 1 else 0)
+
+
+def make_inputs(rank, batch, dev):
+    from pvnet_amd import synth
+    fb = synth.synthetic_batch(batch, seed=1234 + 1000 * rank)
+    seg = torch.from_numpy(fb["seg"]).to(dev)
+    ver = torch.from_numpy(fb["vertex"]).to(dev)
+    return seg, ver, fb
+
+
+def main():
+    args = parse()
+    ws, rank, dev = setup_dist(args)
+    from pvnet_amd import ransac_voting_gpu as rvg
+
+    seg, ver, fb = make_inputs(rank, args.batch, dev)
+    B, K = args.batch, args.steps
+    work = rvg.VotingWorkspace()
+    out = torch.zeros((K, B, VN, 2), dtype=torch.float32, device=dev)
+    diag = {}
+    # correctness guard on the first call: recovered keypoints vs the generator's
+    kp0 = rvg.ransac_voting_layer_v3_from_network(seg, ver, args.hn, _workspace=work, _diag=diag, _seed=1)
+    torch.cuda.synchronize()
+    tn = diag["tn"].cpu().numpy()
+    err = float(np.abs(kp0.cpu().numpy() - fb["keypoints"]).max())
+    if err > 0.5:
+        raise SystemExit(f"keypoint error {err} px > 0.5 on the synthetic field (tn={tn})")
+
+    seeds = [rank * 1_000_003 + 17 * k + 3 for k in range(K)]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    s = torch.cuda.Stream(device=dev)
+    for a, b in ev:       # materialise the hipEvent_t handles before capture
+        a.record(s)
+        b.record(s)
+    torch.cuda.synchronize()
+
+    from pvnet_amd import _lib
+
+    def step(k, timed=True):
+        if timed:   # same call, plus hipEvents around the fused vote+count kernel
+            dd = _lib.V3Diag(ev_vote_begin=ev[k][0].cuda_event, ev_vote_end=ev[k][1].cuda_event)
+            return _raw_v3(rvg, seg, ver, args.hn, seeds[k], work, out[k], dd)
+        return rvg.ransac_voting_layer_v3_from_network(seg, ver, args.hn, _seed=seeds[k], _workspace=work,
+                                                       out=out[k])
+
+    # warmup (eager, also JIT-free: kernels are precompiled)
+    with torch.cuda.stream(s):
+        for i in range(args.warmup):
+            step(i % K, timed=False)
+    torch.cuda.synchronize()
+
+    graph = None
+    if not args.no_graph:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(graph, stream=s):
+                for k in range(K):
+                    step(k)
+        graph.replay()        # one untimed replay (graph upload)
+        torch.cuda.synchronize()
+
+    gathered = torch.zeros((ws, K, B, VN, 2), dtype=torch.float32, device=dev) if ws > 1 else None
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(s):
+        if graph is not None:
+            graph.replay()
+        else:
+            for k in range(K):
+                step(k)
+        if ws > 1:
+            dist.all_gather_into_tensor(gathered, out)     # the stream's single keypoint exchange (RCCL)
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    vote_ms = np.array([a.elapsed_time(b) for a, b in ev])
+    res = dict(elapsed=elapsed, vote_ms=vote_ms, tn=tn)
+    # sanity on the timed outputs
+    final_err = float(np.abs(out.cpu().numpy() - fb["keypoints"][None]).max())
+    if rank == 0:
+        report(args, ws, res, final_err, seg, ver, fb, rvg, work, dev)
+    if ws > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _raw_v3(rvg, seg, ver, hn, seed, work, out, dd):
+    """ransac_voting_layer_v3_from_network with per-kernel timing events."""
+    import ctypes
+    from pvnet_amd import _lib
+    b, c, h, w = ver.shape
+    vertex = ver.permute(0, 2, 3, 1).view(b, h, w, c // 2, 2)
+    d = rvg._desc(seg, vertex, seg=True)
+    prm = rvg._params(hn, 0.99, 0.99, 100, 100, 30000, seed)
+    L = _lib.load()
+    nbytes = L.pv_v3_workspace_size(b, h, w, c // 2, hn)
+    wsb = work.get(ver.device, nbytes)
+    code = L.pv_ransac_voting_v3(ctypes.byref(d), ctypes.byref(prm), out.data_ptr(), wsb.data_ptr(), nbytes,
+                                 ctypes.byref(dd), torch.cuda.current_stream(ver.device).cuda_stream)
+    _lib.check(code, "pv_ransac_voting_v3")
+    return out
+
+
+def measure_u1(dev, hn=512, reps=20):
+    """API-faithful voting_for_hypothesis (dense u8 [hn,vn,tn] write) on one
+    S(1234) image: the kernel the north star's HBM roofline names (U1)."""
+    from pvnet_amd import ransac_voting as rv
+    from pvnet_amd import synth
+    f = synth.synthetic_field(1234)
+    m = np.argmax(f["seg"][0], 0) == 1
+    rows, cols = np.nonzero(m)
+    coords = torch.from_numpy(np.stack([cols, rows], 1).astype(np.float32)).to(dev)
+    direct = torch.from_numpy(np.ascontiguousarray(
+        f["vertex"][0].reshape(VN, 2, H, W)[:, :, rows, cols].transpose(2, 0, 1))).to(dev)
+    tn = coords.shape[0]
+    idxs = torch.randint(0, tn, (hn, VN, 2), dtype=torch.int32, device=dev)
+    hyp = rv.generate_hypothesis(direct, coords, idxs)
+    inl = torch.empty((hn, VN, tn), dtype=torch.uint8, device=dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    rv.voting_for_hypothesis_dense(direct, coords, hyp, inl, 0.99)
+    torch.cuda.synchronize()
+    for a, b in evs:
+        a.record()
+        rv.voting_for_hypothesis_dense(direct, coords, hyp, inl, 0.99)
+        b.record()
+    torch.cuda.synchronize()
+    ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    nbytes = 8 * tn * VN + 8 * tn + 8 * hn * VN + hn * VN * tn      # BASELINE.md U1 algorithmic bytes
+    return dict(kernel="k_vote_bytes<DENSE> (pv_voting_for_hypothesis)", bytes_per_launch=nbytes,
+                ms=ms, achieved_gbs=nbytes / (ms * 1e-3) / 1e9, peak_gbs=HBM_PEAK_GBS,
+                frac=nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, hn=hn, tn=tn)
+
+
+def measure_e2e(dev, seg_dtype=torch.float32, iters=10):
+    """configs[1]: ResNet-18 seg+vector-field forward (PyTorch-ROCm, MIOpen) +
+    the HIP v3 layer on one 480x640 image, eager, random-init weights."""
+    from pvnet_amd import ransac_voting_gpu as rvg
+    from pvnet_amd.network import PVNet
+    torch.manual_seed(0)
+    net = PVNet(18, 2).to(dev).eval().to(memory_format=torch.channels_last)
+    x = torch.randn(1, 3, H, W, device=dev).to(memory_format=torch.channels_last)
+    ws = rvg.VotingWorkspace()
+
+    def once():
+        with torch.no_grad(), torch.autocast("cuda", dtype=seg_dtype, enabled=seg_dtype != torch.float32):
+            s, v = net(x)
+        return rvg.ransac_voting_layer_v3_from_network(s.contiguous(), v.contiguous(), 512, _workspace=ws,
+                                                       max_num=30000)
+    for _ in range(3):
+        once()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        once()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / iters
+    return dict(images_per_s=1.0 / dt, ms_per_image=dt * 1e3, backbone_dtype=str(seg_dtype).replace("torch.", ""),
+                note="random-init weights: foreground from an untrained net is arbitrary; timing only")
+
+
+def cpu_baseline(budget_s):
+    """The oracle's v3 (C kernels, OpenMP) on the host cores, on a bounded
+    sample of the same workload (S(1234), hn=512)."""
+    from oracle import oracle as O
+    from pvnet_amd import synth
+    f = synth.synthetic_field(1234)
+    mask = np.argmax(f["seg"], 1)
+    vertex = np.ascontiguousarray(f["vertex"].transpose(0, 2, 3, 1).reshape(1, H, W, VN, 2))
+    threads = min(16, os.cpu_count() or 1)
+    n, t0 = 0, time.perf_counter()
+    orig = O.vote_counts
+
+    def vc(direct, coords, hyp, thr, nthreads=0):
+        return orig(direct, coords, hyp, thr, nthreads=threads)
+    O.vote_counts = vc
+    try:
+        while True:
+            O.ransac_voting_layer_v3(mask, vertex, 512, seed=n)
+            n += 1
+            if time.perf_counter() - t0 > budget_s:
+                break
+    finally:
+        O.vote_counts = orig
+    dt = time.perf_counter() - t0
+    return dict(value=n / dt, unit="images/sec", cores=threads, kind="port",
+                sample=f"{n} x S(1234) 480x640 fields, tn=29861, hn=512, v3 incl. compaction+refine "
+                       f"(oracle/pvvote_oracle.c, OpenMP {threads} threads)")
+
+
+def report(args, ws, res, final_err, seg, ver, fb, rvg, work, dev):
+    K, B = args.steps, args.batch
+    elapsed = res["elapsed"]
+    value = ws * K * B / elapsed
+    tn = res["tn"]
+    vote_ms = float(np.mean(res["vote_ms"]))
+    pairs = float(args.hn * VN * tn.sum())          # per launch: one launch votes the whole local batch
+    flops = 12.0 * pairs                            # 12 FLOP per (h,v,t)
+    achieved = flops / (vote_ms * 1e-3) / 1e12
+    roof = dict(bound="valu", kernel="k_vote_count (fused vote+count, U2)", achieved=round(achieved, 2),
+                peak=FP32_VECTOR_PEAK_TFLOPS, unit="TFLOP/s", frac=round(achieved / FP32_VECTOR_PEAK_TFLOPS, 4),
+                traffic=None, avg_kernel_ms=round(vote_ms, 5), flop_per_launch=flops,
+                note="12 FLOP per (hypothesis, keypoint, pixel) pair (SURVEY 8(d) U2); HBM traffic per launch "
+                     "~2.4 MB (no inlier mask), so the bound is the vector ALU, not HBM or MFMA")
+    line = {
+        "metric": "images/sec (480x640, 9 kp) vote->keypoint",
+        "value": round(value, 2),
+        "unit": "images/sec",
+        "n_gpus": ws,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / K * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic S(seed) fields (SURVEY 8(d)): disk r=97.5 -> 29,861 fg px, 9 kp, 0.05 rad noise, "
+                "20% outliers; network layout seg_pred/vertex_pred resident in HBM",
+        "config": {"workload": "LINEMOD-cat-sized frame, batch=%d per GPU: ransac_voting_layer_v3 "
+                               "(hn=%d, thr=0.99) from seg_pred/vertex_pred, hipGraph of %d steps" % (B, args.hn, K),
+                   "global_batch": B * ws, "image": [H, W], "keypoints": VN, "round_hyp_num": args.hn,
+                   "foreground_px": int(tn[0]), "parallelism": "dp%d (images sharded, RCCL gather)" % ws},
+        "roofline": roof,
+        "max_kp_err_px": round(final_err, 5),
+    }
+    if not args.skip_u1:
+        try:
+            line["roofline_u1"] = measure_u1(dev, args.hn)
+        except Exception as e:  # reported, never hides the main number
+            line["roofline_u1"] = {"error": repr(e)}
+    if not args.skip_e2e:
+        try:
+            line["e2e_config1"] = measure_e2e(dev)
+        except Exception as e:
+            line["e2e_config1"] = {"error": repr(e)}
+    if ws == 1 and not args.skip_cpu:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,145 @@
+/*
+ * pvvote.h -- C ABI of libpvvote.so, the MI355X (gfx950) implementation of
+ * PVNet's pixel-wise RANSAC keypoint voting.
+ *
+ * Reference interface being replaced (kennege/pvnet):
+ *   lib/ransac_voting_gpu_layer/src/ransac_voting.cpp        (BND)  pybind11 module `ransac_voting`
+ *   lib/ransac_voting_gpu_layer/src/ransac_voting_kernel.cu  (KU)   launchers + kernels
+ *   lib/ransac_voting_gpu_layer/ransac_voting_gpu.py         (RV)   Python voting layers
+ *
+ * Conventions
+ *   - Every pointer is a DEVICE pointer (hipMalloc / torch CUDA tensor memory)
+ *     unless the comment says otherwise.  Sizes are element counts.
+ *   - Every call is asynchronous on `stream` (a hipStream_t; NULL = the null
+ *     stream) and performs no allocation and no host synchronisation, so the
+ *     calls can be captured into a hipGraph.
+ *   - Return value: 0 on success; a positive hipError_t from the launch; or a
+ *     negative PV_E* code for a bad argument.  Nothing ever calls exit()
+ *     (the reference's gpuAssert does, cuda_common.h:19-26).
+ *   - Numerics: fp32 IEEE, no contraction, correctly rounded sqrt/div on every
+ *     decision the reference makes; results are bit-identical to the
+ *     reference arithmetic (see DESIGN.md "Exactness of the fast vote test").
+ */
+#ifndef PVVOTE_H_
+#define PVVOTE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *pv_stream_t; /* hipStream_t */
+
+#define PV_OK 0
+#define PV_EINVAL (-1)     /* bad size / pointer / enum */
+#define PV_EWORKSPACE (-2) /* workspace missing or too small */
+#define PV_EALIGN (-3)     /* pointer not aligned as documented */
+
+/* mask / segmentation encodings accepted by the pipelines */
+#define PV_MASK_I64 0      /* int64 [b,H,W]; v3: (uint8)m != 0 (RV:533 .byte()); EVD: m == 1 (RV:340) */
+#define PV_MASK_U8 1       /* uint8/bool [b,H,W]; same predicates on the byte value */
+#define PV_MASK_I32 2      /* int32 [b,H,W] */
+#define PV_MASK_SEG_F32 3  /* seg_pred logits f32 [b,2,H,W]: argmax(seg,1)==1 fused (DEMO:52) */
+#define PV_MASK_SEG_F16 4  /* seg_pred logits f16 [b,2,H,W] */
+
+#define PV_VERTEX_F32 0
+#define PV_VERTEX_F16 1
+
+#define PV_VOTE_OR 0       /* reference semantics: set 1 where inlier, leave other bytes (KU:124-125) */
+#define PV_VOTE_DENSE 1    /* overwrite every byte with 0/1 (identical for the zero tensors every RV call site passes) */
+
+const char *pv_version(void);
+const char *pv_error_string(int code);
+int pv_device_arch(char *buf, int len); /* writes the gcnArchName of the current device (host pointer) */
+
+/* ---- drop-in kernels: the four functions of the `ransac_voting` module ---- */
+
+/* replaces generate_hypothesis (BND:20-31 -> KU:51-86).
+ * direct f32 [tn,vn,2], coords f32 [tn,2], idxs i32 [hn,vn,2] -> hypo f32 [hn,vn,2]
+ * (every element written; degenerate pairs give (0,0) as the reference's zero-initialised output, KU:75). */
+int pv_generate_hypothesis(const float *direct, const float *coords, const int32_t *idxs, float *hypo,
+                           int32_t tn, int32_t vn, int32_t hn, pv_stream_t stream);
+
+/* replaces voting_for_hypothesis (BND:41-55 -> KU:129-167).
+ * hypo f32 [hn,vn,2]; inliers u8 [hn,vn,tn] caller-owned; mode PV_VOTE_OR or PV_VOTE_DENSE. */
+int pv_voting_for_hypothesis(const float *direct, const float *coords, const float *hypo, uint8_t *inliers,
+                             int32_t tn, int32_t vn, int32_t hn, float inlier_thresh, int32_t mode,
+                             pv_stream_t stream);
+
+/* replaces generate_hypothesis_vanishing_point (BND:64-75 -> KU:231-266); hypo f32 [hn,vn,3]. */
+int pv_generate_hypothesis_vp(const float *direct, const float *coords, const int32_t *idxs, float *hypo,
+                              int32_t tn, int32_t vn, int32_t hn, pv_stream_t stream);
+
+/* replaces voting_for_hypothesis_vanishing_point (BND:85-99 -> KU:313-351); OR semantics. */
+int pv_voting_for_hypothesis_vp(const float *direct, const float *coords, const float *hypo, uint8_t *inliers,
+                                int32_t tn, int32_t vn, int32_t hn, float inlier_thresh, pv_stream_t stream);
+
+/* mask-free form of  inl = zeros(hn,vn,tn); voting_for_hypothesis(...); torch.sum(inl, 2)
+ * (RV:563-567): counts i32 [hn,vn] (overwritten). */
+int pv_vote_counts(const float *direct, const float *coords, const float *hypo, int32_t *counts,
+                   int32_t tn, int32_t vn, int32_t hn, float inlier_thresh, pv_stream_t stream);
+
+/* ---- batched pipelines: the Python layers of RV, fully on device ---- */
+
+typedef struct pv_image_desc {
+    const void *mask;       /* see PV_MASK_*; for SEG_* this is seg_pred */
+    int32_t mask_kind;
+    int64_t mask_strides[4];/* elements: [b,h,w] (unused 4th) or, for SEG_*, [b,c,h,w] */
+    const void *vertex;     /* [b,H,W,vn,2] view, any strides (e.g. vertex_pred.permute(0,2,3,1).view(...)) */
+    int32_t vertex_kind;    /* PV_VERTEX_F32 / PV_VERTEX_F16 */
+    int64_t vertex_strides[5];
+    int32_t b, H, W, vn;
+} pv_image_desc;
+
+typedef struct pv_vote_params {
+    int32_t round_hyp_num;  /* hypotheses per round (RV:520 round_hyp_num) */
+    float inlier_thresh;    /* RV:520 inlier_thresh */
+    float confidence;       /* only sets the diagnostic iteration count */
+    int32_t max_iter;
+    int32_t min_num;        /* fewer foreground pixels -> zeros (RV:537) */
+    int32_t max_num;        /* more -> Bernoulli(max_num/fg) downsampling (RV:543-546) */
+    uint64_t seed;          /* device RNG seed for idxs / downsampling (the reference uses torch's device RNG) */
+    const int32_t *idxs;    /* optional [b, n_hyp, vn, 2] pixel pairs to use instead of the RNG (parity tests) */
+    const uint8_t *keep;    /* optional [b, H, W] downsampling keep-mask instead of the RNG (parity tests) */
+    /* EVD only */
+    int32_t min_hyp_num;    /* RV:333 min_hyp_num (rounds = ceil(min_hyp_num / round_hyp_num)) */
+    int32_t topk;           /* RV:263 topk (estimate_voting_distribution only) */
+} pv_vote_params;
+
+/* optional device outputs for tests/diagnostics (any may be NULL) */
+typedef struct pv_v3_diag {
+    float *hyp;             /* [b, hn, vn, 2] hypotheses */
+    int32_t *counts;        /* [b, vn, hn] inlier counts */
+    int32_t *win_idx;       /* [b, vn] */
+    float *win_ratio;       /* [b, vn] */
+    int32_t *tn;            /* [b] compacted foreground pixels (0 = skipped) */
+    int32_t *iters;         /* [b] iterations the reference's loop would run (RV:578-582) */
+    float *ata;             /* [b, vn, 2, 2] */
+    float *atb;             /* [b, vn, 2] */
+    void *ev_vote_begin;    /* hipEvent_t recorded on `stream` right before / after the fused */
+    void *ev_vote_end;      /* vote+count kernel (per-kernel timing in bench.py)                */
+} pv_v3_diag;
+
+size_t pv_v3_workspace_size(int32_t b, int32_t H, int32_t W, int32_t vn, int32_t n_hyp);
+
+/* ransac_voting_layer_v3 (RV:520-604) for a whole batch; out f32 [b,vn,2]. */
+int pv_ransac_voting_v3(const pv_image_desc *img, const pv_vote_params *prm, float *out,
+                        void *workspace, size_t workspace_bytes, const pv_v3_diag *diag, pv_stream_t stream);
+
+/* estimate_voting_distribution_with_mean (RV:333-406): mean f32 [b,vn,2] (device, input),
+ * cov out f32 [b,vn,2,2].  (The reference returns `mean` unchanged.) */
+int pv_estimate_voting_distribution_with_mean(const pv_image_desc *img, const pv_vote_params *prm,
+                                              const float *mean, float *cov, void *workspace,
+                                              size_t workspace_bytes, pv_stream_t stream);
+
+/* estimate_voting_distribution (RV:263-331): mean out [b,vn,2], cov out [b,vn,2,2].
+ * topk ties at the k-th ratio are taken lowest-hypothesis-index first. */
+int pv_estimate_voting_distribution(const pv_image_desc *img, const pv_vote_params *prm, float *mean,
+                                    float *cov, void *workspace, size_t workspace_bytes, pv_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PVVOTE_H_ */

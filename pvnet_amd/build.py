@@ -1,0 +1,68 @@
+"""Build libpvvote.so (the HIP C-ABI library) in-tree for gfx950.
+
+    python -m pvnet_amd.build            # or __graft_entry__.build()
+
+hipcc cross-compiles without a GPU.  The .so lands next to this file so it
+travels to the GPU box with the repository snapshot.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+SRC = os.path.join(HERE, "csrc", "pvvote.hip")
+HDR = os.path.join(REPO, "include", "pvvote.h")
+OUT = os.path.join(HERE, "libpvvote.so")
+ARCH = os.environ.get("PVVOTE_ARCH", "gfx950")
+
+HIPCC_FLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-shared",
+    # every expression restating reference arithmetic rounds after each op;
+    # the approximate test's FMAs are explicit fmaf() calls
+    "-ffp-contract=off",
+    "-fhip-fp32-correctly-rounded-divide-sqrt",
+    "-fno-gpu-rdc",
+    "-Wall",
+]
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (ROCm install required to build libpvvote.so)")
+
+
+def needs_build() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    return any(os.path.getmtime(p) > t for p in (SRC, HDR, __file__))
+
+
+def build(force: bool = False, extra=()) -> str:
+    if force or needs_build():
+        cmd = [hipcc(), *HIPCC_FLAGS, *extra, "-o", OUT + ".tmp", SRC]
+        subprocess.check_call(cmd)
+        os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+def asm(path: str = os.path.join(HERE, "csrc", "pvvote.gfx950.s")) -> str:
+    """Device assembly for inspection (kernel resource usage, v_cmp/s_bcnt1 loops)."""
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off",
+           "-fhip-fp32-correctly-rounded-divide-sqrt", "--cuda-device-only", "-S", "-o", path, SRC]
+    subprocess.check_call(cmd)
+    return path
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv))

@@ -1,0 +1,141 @@
+"""PVNet seg + vector-field network (ResNet-18 at output stride 8, 3-stage
+upsampling decoder) on PyTorch-ROCm.
+
+Module tree and state-dict keys are those of ``PVnet``
+(lib/networks/model_repository.py:7-79, MR) == ``Resnet18_8s``
+(lib/networks/model_repository_orig.py:7-80), so a reference checkpoint's
+``['net']`` dict loads with ``strict=True``.  Topology (MR:64-79, RN:116-221):
+
+  conv7x7/2 -> BN -> ReLU (x2s) -> maxpool -> layer1 (x4s) -> layer2/2 (x8s)
+  -> layer3 (dilation 2) -> layer4 (dilation 4) -> fc: 3x3 512->256 BN ReLU
+  conv8s(cat[xfc, x8s]) -> up x2 -> conv4s(cat[., x4s]) -> up x2
+  -> conv2s(cat[., x2s]) -> up x2 -> convraw(cat[., image]) -> 1x1 -> seg 2 + vertex 2K
+
+Upsampling is ``UpsamplingBilinear2d`` (align_corners=True) as in MR:35,43,51.
+The convolutions run through MIOpen; ``channels_last`` and fp16/bf16 autocast
+are the MI355X knobs (the reference's fp16 precedent:
+python-only-xin/pvnet-master/tools/train_linemod.py:514).  No weights ship with
+the reference (README.md:101 points to a download), so the default init is the
+reference's own (RN:156-163: He-normal convs, BN weight 1 / bias 0).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import nn
+
+
+def _conv3x3(cin, cout, stride=1, dilation=1):
+    # RN:21-38: padding keeps the spatial size for any dilation
+    return nn.Conv2d(cin, cout, 3, stride=stride, padding=dilation, dilation=dilation, bias=False)
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, cin, cout, stride=1, downsample=None, dilation=1):
+        super().__init__()
+        self.conv1 = _conv3x3(cin, cout, stride, dilation)
+        self.bn1 = nn.BatchNorm2d(cout)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = _conv3x3(cout, cout, dilation=dilation)
+        self.bn2 = nn.BatchNorm2d(cout)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        y = self.relu(self.bn1(self.conv1(x)))
+        y = self.bn2(self.conv2(y))
+        return self.relu(y + idt)
+
+
+class ResNet18OS8(nn.Module):
+    """ResNet-18 whose layer3/layer4 trade stride for dilation (RN:167-198).
+    Keeps the reference's unused ``avgpool`` attribute so the module tree (and
+    therefore the state-dict keys) match."""
+
+    def __init__(self):
+        super().__init__()
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        # (planes, blocks, stride, dilation) after the output-stride rule: OS 8 is
+        # reached after layer2, so layer3/4 keep stride 1 with dilation 2/4.
+        self.layer1 = self._layer(64, 2, 1, 1, False)
+        self.layer2 = self._layer(128, 2, 2, 1, True)
+        self.layer3 = self._layer(256, 2, 1, 2, True)
+        self.layer4 = self._layer(512, 2, 1, 4, True)
+        self.avgpool = nn.AvgPool2d(7, padding=3, stride=1)
+        self.fc = nn.Identity()   # replaced by PVNet (MR:22-26)
+
+    def _layer(self, planes, blocks, stride, dilation, down):
+        ds = None
+        if down:
+            ds = nn.Sequential(nn.Conv2d(self.inplanes, planes, 1, stride=stride, bias=False), nn.BatchNorm2d(planes))
+        mods = [BasicBlock(self.inplanes, planes, stride, ds, dilation)]
+        self.inplanes = planes
+        mods += [BasicBlock(planes, planes, dilation=dilation) for _ in range(1, blocks)]
+        return nn.Sequential(*mods)
+
+    def forward(self, x):
+        x2s = self.relu(self.bn1(self.conv1(x)))
+        x4s = self.layer1(self.maxpool(x2s))
+        x8s = self.layer2(x4s)
+        x16s = self.layer3(x8s)
+        x32s = self.layer4(x16s)
+        return x2s, x4s, x8s, x16s, x32s, self.fc(x32s)
+
+
+def _cbl(cin, cout, leaky=True):
+    return nn.Sequential(nn.Conv2d(cin, cout, 3, 1, 1, bias=False), nn.BatchNorm2d(cout),
+                         nn.LeakyReLU(0.1, True) if leaky else nn.ReLU(True))
+
+
+class PVNet(nn.Module):
+    """``PVnet(ver_dim, seg_dim)`` of MR:7-79 (alias :data:`Resnet18_8s`)."""
+
+    def __init__(self, ver_dim=18, seg_dim=2, fcdim=256, s8dim=128, s4dim=64, s2dim=32, raw_dim=32):
+        super().__init__()
+        self.ver_dim, self.seg_dim = ver_dim, seg_dim
+        r = ResNet18OS8()
+        r.fc = _cbl(512, fcdim, leaky=False)
+        self.resnet18_8s = r
+        self.conv8s = _cbl(128 + fcdim, s8dim)
+        self.up8sto4s = nn.UpsamplingBilinear2d(scale_factor=2)
+        self.conv4s = _cbl(64 + s8dim, s4dim)
+        self.up4sto2s = nn.UpsamplingBilinear2d(scale_factor=2)
+        self.conv2s = _cbl(64 + s4dim, s2dim)
+        self.up2storaw = nn.UpsamplingBilinear2d(scale_factor=2)
+        self.convraw = nn.Sequential(nn.Conv2d(3 + s2dim, raw_dim, 3, 1, 1, bias=False), nn.BatchNorm2d(raw_dim),
+                                     nn.LeakyReLU(0.1, True), nn.Conv2d(raw_dim, seg_dim + ver_dim, 1, 1))
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        """RN:156-163 for every conv / BN (the decoder is built after the
+        backbone in MR, so torch's default init applies there; we use the
+        backbone rule throughout -- no reference weights exist offline)."""
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                n = m.kernel_size[0] * m.kernel_size[1] * m.out_channels
+                m.weight.data.normal_(0, math.sqrt(2.0 / n))
+                if m.bias is not None:
+                    m.bias.data.zero_()
+            elif isinstance(m, nn.BatchNorm2d):
+                m.weight.data.fill_(1)
+                m.bias.data.zero_()
+
+    def forward(self, x):
+        x2s, x4s, x8s, _, _, xfc = self.resnet18_8s(x)
+        fm = self.up8sto4s(self.conv8s(torch.cat([xfc, x8s], 1)))
+        fm = self.up4sto2s(self.conv4s(torch.cat([fm, x4s], 1)))
+        fm = self.up2storaw(self.conv2s(torch.cat([fm, x2s], 1)))
+        x = self.convraw(torch.cat([fm, x], 1))
+        return x[:, :self.seg_dim], x[:, self.seg_dim:]
+
+
+Resnet18_8s = PVNet
+PVnet = PVNet

@@ -1,0 +1,311 @@
+"""Parity of the HIP path (through the C ABI of libpvvote.so) with the CPU
+oracle and the reference's golden vectors.  Bit-exact for hypotheses, inlier
+bytes, counts, winners; tolerances for the fp32 least squares / covariances."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from tests import golden_io as G
+
+pytestmark = pytest.mark.gpu
+
+KP_TOL = 1e-2
+COV_RTOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def rv():
+    from pvnet_amd import ransac_voting
+    return ransac_voting
+
+
+@pytest.fixture(scope="module")
+def rvg():
+    from pvnet_amd import ransac_voting_gpu
+    return ransac_voting_gpu
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def cu(x, dev, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(x))
+    return t.to(dev) if dtype is None else t.to(device=dev, dtype=dtype)
+
+
+def test_native_library_is_the_gfx950_build(device):
+    from pvnet_amd import _lib
+    import ctypes
+    L = _lib.load()
+    buf = ctypes.create_string_buffer(64)
+    assert L.pv_device_arch(buf, 64) == 0
+    assert buf.value.decode().startswith("gfx950"), buf.value
+
+
+# ---------------------------------------------------------------- kernels
+@pytest.mark.parametrize("case", ["cat_v3_512", "synth_v3_512"])
+def test_generate_and_vote_kernels_bit_exact(case, device, rv):
+    g = G.load(case)
+    mask, vertex = (G.cat_inputs(g) if case.startswith("cat") else G.synth_inputs(g))[:2]
+    coords, direct = O.compact(O.fg_mask_v3(mask[0]), vertex[0])
+    idxs = g["idxs"][0]
+    hyp = rv.generate_hypothesis(cu(direct, device), cu(coords, device), cu(idxs, device)).cpu().numpy()
+    np.testing.assert_array_equal(bits(hyp), bits(g["hyp"][0]))
+    cnt = rv.vote_counts(cu(direct, device), cu(coords, device), cu(hyp, device), 0.99).cpu().numpy()
+    np.testing.assert_array_equal(cnt, g["counts"][0])
+    # byte outputs on a slice of hypotheses (the full mask is 137 MB at the synthetic size)
+    hs = slice(0, 64)
+    ref = np.zeros((64, hyp.shape[1], coords.shape[0]), np.uint8)
+    O.voting_for_hypothesis(direct, coords, hyp[hs], ref, 0.99)
+    for dense in (False, True):
+        out = torch.zeros(ref.shape, dtype=torch.uint8, device=device)
+        fn = rv.voting_for_hypothesis_dense if dense else rv.voting_for_hypothesis
+        fn(cu(direct, device), cu(coords, device), cu(hyp[hs], device), out, 0.99)
+        np.testing.assert_array_equal(out.cpu().numpy(), ref)
+        np.testing.assert_array_equal(out.cpu().numpy().sum(2), g["counts"][0][hs])
+
+
+def test_voting_or_semantics_keeps_existing_bytes(device, rv):
+    g = G.load("edge_cases")
+    coords, direct = O.compact(O.fg_mask_v3(g["c_mask"][0]), g["c_vertex"][0])
+    hyp = g["c_hyp"][0]
+    init = (np.random.default_rng(0).random((hyp.shape[0], hyp.shape[1], coords.shape[0])) < 0.3).astype(np.uint8) * 7
+    ref = init.copy()
+    O.voting_for_hypothesis(direct, coords, hyp, ref, 0.99)
+    out = cu(init, device)
+    rv.voting_for_hypothesis(cu(direct, device), cu(coords, device), cu(hyp, device), out, 0.99)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_guard_band_stress(seed, device, rv):
+    """Thresholds placed exactly on reference cosines, degenerate pixels and
+    hypotheses: every byte must still equal the exact reference decision."""
+    rng = np.random.default_rng(seed)
+    tn, vn, hn = 3000, 3, 200
+    coords = np.stack([rng.integers(0, 640, tn), rng.integers(0, 480, tn)], 1).astype(np.float32)
+    ang = rng.uniform(-np.pi, np.pi, (tn, vn))
+    scale = rng.choice([1.0, 1e-7, 3e-7, 0.0, 1e5, 2e19], size=(tn, vn), p=[0.9, 0.02, 0.02, 0.02, 0.02, 0.02])
+    direct = np.stack([np.cos(ang) * scale, np.sin(ang) * scale], -1).astype(np.float32)
+    hyp = np.stack([rng.uniform(-100, 700, (hn, vn)), rng.uniform(-100, 600, (hn, vn))], -1).astype(np.float32)
+    hyp[:10] = np.round(hyp[:10])                      # exactly on pixel centres / lattice
+    hyp[10:12] = coords[rng.integers(0, tn, (2, vn))]  # exactly on foreground pixels
+    hyp[12, :, 0] = 1e20                               # outside the fast domain
+    hyp[13] = np.nan
+    # thresholds equal to actual reference cosines (pairs land exactly on them)
+    d = hyp[20, 0] - coords[5]
+    for thr in (0.99, float(np.float32(np.dot(d, direct[5, 0]) / (np.linalg.norm(d) * np.linalg.norm(direct[5, 0])))),
+                0.0, -0.5, 0.999999):
+        ref = np.zeros((hn, vn, tn), np.uint8)
+        O.voting_for_hypothesis(direct, coords, hyp, ref, thr)
+        out = torch.zeros(ref.shape, dtype=torch.uint8, device=device)
+        rv.voting_for_hypothesis_dense(cu(direct, device), cu(coords, device), cu(hyp, device), out, thr)
+        np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"thr={thr}")
+        cnt = rv.vote_counts(cu(direct, device), cu(coords, device), cu(hyp, device), thr).cpu().numpy()
+        np.testing.assert_array_equal(cnt, ref.sum(2), err_msg=f"thr={thr}")
+
+
+def test_vp_kernels(device, rv):
+    g = G.load("vp_kernels")
+    hyp = rv.generate_hypothesis_vanishing_point(cu(g["direct"], device), cu(g["coords"], device),
+                                                 cu(g["idxs"], device))
+    np.testing.assert_array_equal(bits(hyp.cpu().numpy()), bits(g["hyp"]))
+    inl = torch.zeros(g["inliers"].shape, dtype=torch.uint8, device=device)
+    rv.voting_for_hypothesis_vanishing_point(cu(g["direct"], device), cu(g["coords"], device), hyp, inl, 0.99)
+    np.testing.assert_array_equal(inl.cpu().numpy(), g["inliers"])
+
+
+def test_input_checks(device, rv):
+    d = torch.zeros(10, 3, 2, device=device)
+    c = torch.zeros(10, 2, device=device)
+    i = torch.zeros(4, 3, 2, dtype=torch.int32, device=device)
+    with pytest.raises(RuntimeError, match="CUDA"):
+        rv.generate_hypothesis(d.cpu(), c, i)
+    with pytest.raises(RuntimeError, match="contiguous"):
+        rv.generate_hypothesis(d.transpose(0, 1), c, i)
+
+
+# ---------------------------------------------------------------- v3 pipeline
+def run_v3(rvg, mask, vertex, g, prefix, device, hn=None, keep=None, **kw):
+    idxs_g = g[prefix + "idxs"]
+    b = mask.shape[0]
+    fg = [int(O.fg_mask_v3(m).sum()) for m in mask]
+    voted = [i for i, n in enumerate(fg) if n >= kw.get("min_num", 100)]
+    hn = hn or idxs_g.shape[1]
+    idxs = np.zeros((b, hn) + idxs_g.shape[2:], np.int32)
+    for k, i in enumerate(voted):
+        idxs[i] = idxs_g[k]
+    diag = {}
+    kp = rvg.ransac_voting_layer_v3(cu(mask, device), cu(vertex, device), hn, _idxs=idxs, _keep=keep,
+                                    _diag=diag, **kw).cpu().numpy()
+    diag = {k: v.cpu().numpy() for k, v in diag.items()}
+    for k, i in enumerate(voted):
+        np.testing.assert_array_equal(bits(diag["hyp"][i]), bits(g[prefix + "hyp"][k]))
+        np.testing.assert_array_equal(diag["counts"][i].T, g[prefix + "counts"][k])
+        np.testing.assert_array_equal(diag["win_idx"][i], np.argmax(g[prefix + "counts"][k], 0))
+    for i in range(b):
+        if i not in voted:
+            assert diag["tn"][i] == 0 and np.all(kp[i] == 0)
+    np.testing.assert_allclose(kp, g[prefix + "keypoints"], atol=KP_TOL, rtol=0)
+    return kp, diag
+
+
+def test_v3_cat_known_answer(device, rvg):
+    g = G.load("cat_v3_512")
+    mask, vertex, _ = G.cat_inputs(g)
+    kp, diag = run_v3(rvg, mask, vertex, g, "", device)
+    assert np.abs(kp[0] - g["points_2d"]).max() < 1e-3
+    assert int(diag["iters"][0]) == int(g["iters"])
+
+
+def test_v3_cat_downsampled(device, rvg):
+    g = G.load("cat_v3_128_maxnum100")
+    mask, vertex, _ = G.cat_inputs(g)
+    keep = np.unpackbits(g["keep_bits"][0])[: 480 * 640].reshape(1, 480, 640)
+    run_v3(rvg, mask, vertex, g, "", device, keep=keep, max_num=100)
+
+
+@pytest.mark.parametrize("hn", [512, 128])
+def test_v3_synth_full_size(hn, device, rvg):
+    g = G.load(f"synth_v3_{hn}")
+    mask, vertex, _ = G.synth_inputs(g)
+    kp, diag = run_v3(rvg, mask, vertex, g, "", device)
+    assert int(diag["tn"][0]) == 29861
+    assert int(diag["iters"][0]) == int(g["iters"])
+
+
+def test_v3_from_network_fused(device, rvg):
+    """seg_pred/vertex_pred straight from the network layout (argmax fused)."""
+    g = G.load("synth_v3_512")
+    _, _, f = G.synth_inputs(g)
+    idxs = g["idxs"]
+    for dt in (torch.float32, torch.float16):
+        seg = cu(f["seg"], device, dt)
+        ver = cu(f["vertex"], device, dt)
+        diag = {}
+        kp = rvg.ransac_voting_layer_v3_from_network(seg, ver, 512, _idxs=idxs, _diag=diag).cpu().numpy()
+        if dt == torch.float32:
+            np.testing.assert_array_equal(bits(diag["hyp"].cpu().numpy()[0]), bits(g["hyp"][0]))
+            np.testing.assert_array_equal(diag["counts"].cpu().numpy()[0].T, g["counts"][0])
+            np.testing.assert_allclose(kp, g["keypoints"], atol=KP_TOL, rtol=0)
+        else:
+            # fp16 network outputs: compare with the oracle on the same (rounded) field
+            v16 = f["vertex"].astype(np.float16).astype(np.float32)
+            vv = np.ascontiguousarray(v16.transpose(0, 2, 3, 1).reshape(1, 480, 640, 9, 2))
+            dg = []
+            ko = O.ransac_voting_layer_v3(np.argmax(f["seg"], 1), vv, 512, idxs=[idxs[0]], diag=dg)
+            np.testing.assert_array_equal(diag["counts"].cpu().numpy()[0].T, dg[0]["counts"])
+            np.testing.assert_allclose(kp, ko, atol=KP_TOL, rtol=0)
+
+
+def test_v3_edge_cases(device, rvg):
+    g = G.load("edge_cases")
+    run_v3(rvg, g["a_mask"], g["a_vertex"], g, "a_", device)
+    kp, diag = run_v3(rvg, g["b_mask"], g["b_vertex"], g, "b_", device)
+    assert int(diag["iters"][0]) == int(g["b_iters"]) == 101
+    np.testing.assert_allclose(kp[0], diag["atb"][0], rtol=1e-6)     # b_inv identity fallback
+    run_v3(rvg, g["c_mask"], g["c_vertex"], g, "c_", device)
+    run_v3(rvg, g["d_mask"], g["d_vertex"], g, "d_", device, keep=g["d_keep"].astype(np.uint8), max_num=300)
+    run_v3(rvg, g["e_mask"], g["e_vertex"], g, "e_", device, inlier_thresh=0.999)
+
+
+def test_v3_mask_dtypes_and_contiguous_vertex(device, rvg):
+    g = G.load("edge_cases")
+    m = g["a_mask"]
+    base, _ = run_v3(rvg, m, g["a_vertex"], g, "a_", device)
+    for conv in (lambda x: x.astype(np.int32), lambda x: (x & 0xFF).astype(np.uint8)):
+        kp, _ = run_v3(rvg, conv(m), g["a_vertex"], g, "a_", device)
+        np.testing.assert_array_equal(kp, base)
+
+
+def test_v3_rng_path_statistical(device, rvg):
+    """Device RNG instead of injected idxs: results agree with the oracle's
+    (different random draws) within the north star's 0.5 px."""
+    g = G.load("synth_v3_512")
+    mask, vertex, f = G.synth_inputs(g)
+    torch.manual_seed(0)
+    kp = rvg.ransac_voting_layer_v3(cu(mask, device), cu(vertex, device), 512).cpu().numpy()
+    np.testing.assert_allclose(kp, g["keypoints"], atol=0.5)
+    gc = G.load("cat_v3_512")
+    mc, vc, _ = G.cat_inputs(gc)
+    kc = rvg.ransac_voting_layer_v3(cu(mc, device), cu(vc, device), 512).cpu().numpy()
+    assert np.abs(kc[0] - gc["points_2d"]).max() < 1e-3
+
+
+def test_v3_batch_matches_single(device, rvg):
+    """8 synthetic images in one batched call == 8 single calls (same idxs)."""
+    from pvnet_amd import synth
+    fb = synth.synthetic_batch(4, seed=100)
+    mask = np.argmax(fb["seg"], 1)
+    vertex = np.ascontiguousarray(fb["vertex"].transpose(0, 2, 3, 1).reshape(4, 480, 640, 9, 2))
+    idxs = np.random.default_rng(3).integers(0, 29861, (4, 128, 9, 2)).astype(np.int32)
+    kb = rvg.ransac_voting_layer_v3(cu(mask, device), cu(vertex, device), 128, _idxs=idxs).cpu().numpy()
+    for i in range(4):
+        k1 = rvg.ransac_voting_layer_v3(cu(mask[i:i + 1], device), cu(vertex[i:i + 1], device), 128,
+                                        _idxs=idxs[i:i + 1]).cpu().numpy()
+        np.testing.assert_array_equal(kb[i], k1[0])
+        ko = O.ransac_voting_layer_v3(mask[i:i + 1], vertex[i:i + 1], 128, idxs=[idxs[i]])
+        np.testing.assert_allclose(kb[i], ko[0], atol=KP_TOL)
+        np.testing.assert_allclose(kb[i], fb["keypoints"][i], atol=0.5)
+
+
+# ---------------------------------------------------------------- EVD
+@pytest.mark.parametrize("case", ["cat_evdm", "synth_evdm"])
+def test_evd_with_mean(case, device, rvg):
+    g = G.load(case)
+    mask, vertex = (G.cat_inputs(g) if case.startswith("cat") else G.synth_inputs(g))[:2]
+    idxs = g["idxs"][0].reshape(1, -1, 9, 2)
+    _, cov = rvg.estimate_voting_distribution_with_mean(cu(mask, device), cu(vertex, device), cu(g["mean"], device),
+                                                        _idxs=idxs)
+    cov = cov.cpu().numpy()
+    np.testing.assert_allclose(cov, g["cov"], rtol=COV_RTOL, atol=1e-4 * np.abs(g["cov"]).max())
+
+
+def test_evd_edge_batch(device, rvg):
+    g = G.load("edge_cases")
+    idx = g["a_evdm_idxs"]
+    idxs = np.stack([idx[0:4].reshape(-1, 3, 2), idx[4:8].reshape(-1, 3, 2), idx[8:12].reshape(-1, 3, 2)])
+    _, cov = rvg.estimate_voting_distribution_with_mean(cu(g["a_mask"], device), cu(g["a_vertex"], device),
+                                                        cu(g["a_keypoints"], device), round_hyp_num=32,
+                                                        min_hyp_num=100, _idxs=idxs)
+    np.testing.assert_allclose(cov.cpu().numpy(), g["a_evdm_cov"], rtol=COV_RTOL,
+                               atol=1e-4 * np.abs(g["a_evdm_cov"]).max())
+
+
+def test_evd_topk(device, rvg):
+    g = G.load("synth_evd_top4096")
+    mask, vertex, _ = G.synth_inputs(g)
+    idxs = g["idxs"][0].reshape(1, -1, 9, 2)
+    mu, cov = rvg.estimate_voting_distribution(cu(mask, device), cu(vertex, device), topk=4096, _idxs=idxs)
+    np.testing.assert_allclose(mu.cpu().numpy(), g["mean"], atol=1e-3, rtol=1e-5)
+    np.testing.assert_allclose(cov.cpu().numpy(), g["cov"], rtol=COV_RTOL, atol=1e-4 * np.abs(g["cov"]).max())
+    g = G.load("synth_evd_top128")
+    idxs = g["idxs"][0].reshape(1, -1, 9, 2)
+    mu, cov = rvg.estimate_voting_distribution(cu(mask, device), cu(vertex, device), topk=128, _idxs=idxs)
+    mo, co = O.estimate_voting_distribution(mask, vertex, topk=128, idxs=[list(g["idxs"][0])])
+    np.testing.assert_allclose(mu.cpu().numpy(), mo, atol=1e-3, rtol=1e-5)
+    np.testing.assert_allclose(cov.cpu().numpy(), co, rtol=COV_RTOL, atol=1e-4 * np.abs(co).max())
+
+
+def test_graph_capture(device, rvg):
+    """The whole v3 pipeline is capturable in a hipGraph and replays exactly."""
+    from pvnet_amd import synth
+    f = synth.synthetic_field(7)
+    seg = cu(f["seg"], device)
+    ver = cu(f["vertex"], device)
+    ws = rvg.VotingWorkspace()
+    out = torch.empty((1, 9, 2), device=device)
+    rvg.ransac_voting_layer_v3_from_network(seg, ver, 128, _seed=5, _workspace=ws, out=out)
+    ref = out.clone()
+    torch.cuda.synchronize()
+    gph = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(gph, stream=s):
+            rvg.ransac_voting_layer_v3_from_network(seg, ver, 128, _seed=5, _workspace=ws, out=out)
+    out.zero_()
+    gph.replay()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), ref.cpu().numpy())
