@@ -29,6 +29,9 @@ HIPCC_FLAGS = [
     # the approximate test's FMAs are explicit fmaf() calls
     "-ffp-contract=off",
     "-fhip-fp32-correctly-rounded-divide-sqrt",
+    # packed f32 (v_pk_*) has no throughput advantage on gfx950 and costs
+    # the abs/neg source modifiers the vote test relies on
+    "-fno-slp-vectorize",
     "-fno-gpu-rdc",
     "-Wall",
 ]
@@ -58,8 +61,8 @@ def build(force: bool = False, extra=()) -> str:
 
 def asm(path: str = os.path.join(HERE, "csrc", "pvvote.gfx950.s")) -> str:
     """Device assembly for inspection (kernel resource usage, v_cmp/s_bcnt1 loops)."""
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off",
-           "-fhip-fp32-correctly-rounded-divide-sqrt", "--cuda-device-only", "-S", "-o", path, SRC]
+    cmd = [hipcc(), *[f for f in HIPCC_FLAGS if f not in ("-shared", "-fPIC", "-Wall")],
+           "--cuda-device-only", "-S", "-o", path, SRC]
     subprocess.check_call(cmd)
     return path
 

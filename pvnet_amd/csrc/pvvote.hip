@@ -37,11 +37,11 @@
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kCompactChunk = 4096;          // pixels per compaction block (256 threads x 16)
+constexpr int kCompactChunk = 1024;          // pixels per compaction block (256 threads x 4)
 constexpr int kVotePix = 4;                  // pixels per lane in the vote waves
 constexpr int kVoteChunk = kWave * kVotePix; // 256 pixels per vote item
-constexpr int kVoteHG = 128;                 // hypotheses per vote item
 constexpr int kRefineNJ = 16;                // refine blocks per (image, keypoint)
+constexpr int kBytesHG = 128;                // hypotheses per item of the byte-output vote kernel
 // |fast - reference| <= 15 ulp(1) ~ 9e-7; the band is 4.4x wider.
 constexpr float kGuard = 4.0e-6f;
 // domain of the fast test's error bound
@@ -140,8 +140,16 @@ __host__ __device__ inline uint64_t mix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
+// 32-bit avalanche (lowbias32 constants); two rounds keyed by the seed
+__host__ __device__ inline uint32_t hash32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du;
+    x ^= x >> 15; x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
 __device__ inline int32_t rand_index(uint64_t seed, uint64_t key, int32_t n) {
-    uint32_t r = (uint32_t)(mix64(seed ^ mix64(key)) >> 32);
+    uint32_t r = hash32(hash32((uint32_t)key ^ (uint32_t)seed) + (uint32_t)(key >> 32) + (uint32_t)(seed >> 32));
     return (int32_t)(((uint64_t)r * (uint32_t)n) >> 32);
 }
 
@@ -189,23 +197,20 @@ __device__ __forceinline__ bool is_fg(const MaskView &m, int b, int r, int c) {
 // workspace
 // --------------------------------------------------------------------------
 struct Workspace {
-    // zeroed every call (one memset)
-    int32_t *fg;        // [b] raw foreground count
-    int32_t *tnds;      // [b] count after downsampling
-    int32_t *counts;    // [b][vn][nh]
-    size_t zero_bytes;
-    // written before read
+    int32_t *counts;    // [b][vn][nh]   zeroed by k_fg_count
+    int32_t *ticket;    // [b]           zeroed by k_fg_count
+    uint32_t *exotic;   // [b][nchv]     zeroed by k_fg_count (chunk holds a pixel outside the fast domain)
+    int64_t nchv;       // vote chunks per image (capacity)
+    int64_t zero_words; // counts + ticket + exotic (contiguous)
     int32_t *tn;        // [b] compacted pixels (0 = image skipped)
-    int32_t *item_base; // [b+1] vote items prefix
+    int32_t *fgtot;     // [b] foreground before downsampling
     int32_t *blkcnt;    // [b][nblk]
     int32_t *dscnt;     // [b][nblk]
-    float2 *coords;     // [b][P]
-    float2 *raw;        // [b][vn][P]
+    float4 *pex;        // [b][vn][P]   exact pixel data (cx, cy, nx, ny): reference operands
+    float4 *pix;        // [b][vn][P]   fast-test data (fx, cy, ux, uy)
     float2 *hyp;        // [b][nh][vn]  (reference layout)
-    float2 *hypf;       // [b][vn][nh]  fast copy, NaN = exact-only
     int32_t *win;       // [b][vn]
     float *ratio;       // [b][vn]
-    float2 *best;       // [b][vn]
     double *refpart;    // [b][vn][kRefineNJ][5]
     size_t total;
 };
@@ -217,21 +222,20 @@ Workspace carve(void *base, int b, int H, int W, int vn, int nh) {
     char *p = (char *)base;
     int64_t off = 0;
     auto take = [&](int64_t bytes) { char *q = p ? p + off : nullptr; off = align_up(off + bytes, 256); return q; };
-    w.fg = (int32_t *)take(4 * b);
-    w.tnds = (int32_t *)take(4 * b);
-    w.counts = (int32_t *)take(4 * (int64_t)b * vn * nh);
-    w.zero_bytes = (size_t)off;
+    w.nchv = (P + kVoteChunk - 1) / kVoteChunk;
+    w.zero_words = (int64_t)b * vn * nh + b + b * w.nchv;
+    w.counts = (int32_t *)take(4 * w.zero_words);
+    w.ticket = w.counts ? w.counts + (int64_t)b * vn * nh : nullptr;
+    w.exotic = w.counts ? (uint32_t *)(w.ticket + b) : nullptr;
     w.tn = (int32_t *)take(4 * b);
-    w.item_base = (int32_t *)take(4 * (b + 1));
+    w.fgtot = (int32_t *)take(4 * b);
     w.blkcnt = (int32_t *)take(4 * b * nblk);
     w.dscnt = (int32_t *)take(4 * b * nblk);
-    w.coords = (float2 *)take(8 * b * P);
-    w.raw = (float2 *)take(8 * b * vn * P);
+    w.pex = (float4 *)take(16 * b * vn * P);
+    w.pix = (float4 *)take(16 * b * vn * P);
     w.hyp = (float2 *)take(8 * (int64_t)b * nh * vn);
-    w.hypf = (float2 *)take(8 * (int64_t)b * nh * vn);
     w.win = (int32_t *)take(4 * b * vn);
     w.ratio = (float *)take(4 * b * vn);
-    w.best = (float2 *)take(8 * b * vn);
     w.refpart = (double *)take(8 * 5 * (int64_t)b * vn * kRefineNJ);
     w.total = (size_t)off;
     return w;
@@ -248,62 +252,76 @@ __device__ __forceinline__ double wave_sum_d(double x) {
     for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
     return x;
 }
-
-// ==========================================================================
-// K1: foreground count per 4096-pixel block (and per image, atomically)
-// ==========================================================================
-template <int KIND, bool EVD>
-__global__ __launch_bounds__(256) void k_fg_count(MaskView m, int H, int W, int32_t *blkcnt, int32_t *fg, int nblk) {
-    const int b = blockIdx.y, blk = blockIdx.x;
-    const int64_t P = (int64_t)H * W;
-    __shared__ int wsum[4];
-    int c = 0;
-#pragma unroll 4
-    for (int k = 0; k < kCompactChunk / 256; ++k) {
-        int64_t p = (int64_t)blk * kCompactChunk + k * 256 + threadIdx.x;
-        bool f = false;
-        if (p < P) f = is_fg<KIND, EVD>(m, b, (int)(p / W), (int)(p % W));
-        c += f;
-    }
-    c = wave_sum_i(c);
-    if (lane_id() == 0) wsum[threadIdx.x / 64] = c;
+// sum over the block of (x, y); `sh` holds >= 8 ints
+__device__ __forceinline__ int2 block_sum2(int x, int y, int *sh) {
+    x = wave_sum_i(x);
+    y = wave_sum_i(y);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        int t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-        blkcnt[b * nblk + blk] = t;
-        if (t) atomicAdd(&fg[b], t);
-    }
+    if (lane_id() == 0) { sh[threadIdx.x / 64] = x; sh[4 + threadIdx.x / 64] = y; }
+    __syncthreads();
+    return make_int2(sh[0] + sh[1] + sh[2] + sh[3], sh[4] + sh[5] + sh[6] + sh[7]);
 }
 
-// K1b: recount with the Bernoulli(max_num/fg) selection (RV:543-546, RV:351-355).
+// ==========================================================================
+// K1: foreground count per 1024-pixel block; zeroes the pipeline's counters
+// ==========================================================================
 template <int KIND, bool EVD>
-__global__ __launch_bounds__(256) void k_fg_downsample(MaskView m, int H, int W, const int32_t *fg, int32_t *dscnt,
-                                                       int32_t *tnds, int nblk, int min_num, int max_num,
+__global__ __launch_bounds__(256) void k_fg_count(MaskView m, int H, int W, int32_t *blkcnt, int nblk,
+                                                  int32_t *zero, int64_t zero_words) {
+    const int b = blockIdx.y, blk = blockIdx.x;
+    const int64_t P = (int64_t)H * W;
+    {   // zero counts + tickets (read only by later kernels of this pipeline)
+        int64_t g = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x;
+        int64_t G = (int64_t)gridDim.x * gridDim.y * 256;
+        for (int64_t i = g; i < zero_words; i += G) zero[i] = 0;
+    }
+    __shared__ int sh[8];
+    bool f[kCompactChunk / 256];
+#pragma unroll
+    for (int k = 0; k < kCompactChunk / 256; ++k) {
+        int64_t p = (int64_t)blk * kCompactChunk + k * 256 + threadIdx.x;
+        f[k] = p < P && is_fg<KIND, EVD>(m, b, (int)(p / W), (int)(p % W));
+    }
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < kCompactChunk / 256; ++k) c += f[k];
+    int2 t = block_sum2(c, 0, sh);
+    if (threadIdx.x == 0) blkcnt[b * nblk + blk] = t.x;
+}
+
+// foreground total of image b from the per-block counts (every block of K1b/K2 does this)
+__device__ __forceinline__ int2 image_totals(const int32_t *cnt, int nblk, int upto, int *sh) {
+    int all = 0, pre = 0;
+    for (int j = threadIdx.x; j < nblk; j += 256) {
+        int v = cnt[j];
+        all += v;
+        pre += j < upto ? v : 0;
+    }
+    return block_sum2(all, pre, sh);
+}
+
+// K1b: recount with the Bernoulli(max_num/fg) selection (RV:543-546, RV:351-355);
+// exits at once for images that need none (the common case).
+template <int KIND, bool EVD>
+__global__ __launch_bounds__(256) void k_fg_downsample(MaskView m, int H, int W, const int32_t *blkcnt,
+                                                       int32_t *dscnt, int nblk, int min_num, int max_num,
                                                        uint64_t seed, const uint8_t *keep) {
     const int b = blockIdx.y, blk = blockIdx.x;
-    const int fgb = fg[b];
+    __shared__ int sh[8];
+    const int fgb = image_totals(blkcnt + b * nblk, nblk, 0, sh).x;
     if (fgb < min_num || fgb <= max_num) return;
     const int64_t P = (int64_t)H * W;
     const float thr = (float)max_num / (float)fgb;
-    __shared__ int wsum[4];
     int c = 0;
+#pragma unroll
     for (int k = 0; k < kCompactChunk / 256; ++k) {
         int64_t p = (int64_t)blk * kCompactChunk + k * 256 + threadIdx.x;
-        bool f = false;
-        if (p < P) {
-            f = is_fg<KIND, EVD>(m, b, (int)(p / W), (int)(p % W));
-            if (f) f = keep ? keep[b * P + p] != 0 : rand_unit(seed, (uint64_t)b * P + p) < thr;
-        }
+        bool f = p < P && is_fg<KIND, EVD>(m, b, (int)(p / W), (int)(p % W));
+        if (f) f = keep ? keep[b * P + p] != 0 : rand_unit(seed, (uint64_t)b * P + p) < thr;
         c += f;
     }
-    c = wave_sum_i(c);
-    if (lane_id() == 0) wsum[threadIdx.x / 64] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-        dscnt[b * nblk + blk] = t;
-        if (t) atomicAdd(&tnds[b], t);
-    }
+    int2 t = block_sum2(c, 0, sh);
+    if (threadIdx.x == 0) dscnt[b * nblk + blk] = t.x;
 }
 
 // ==========================================================================
@@ -319,313 +337,466 @@ struct VertexView {
 };
 
 template <int KIND, bool EVD>
-__global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int H, int W, int vn, const int32_t *fg,
-                                                 const int32_t *tnds, const int32_t *blkcnt, const int32_t *dscnt,
-                                                 int nblk, int min_num, int max_num, uint64_t seed, const uint8_t *keep,
-                                                 int32_t *tn, float2 *coords, float2 *raw) {
+__global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int H, int W, int vn,
+                                                 const int32_t *blkcnt, const int32_t *dscnt, int nblk, int min_num,
+                                                 int max_num, uint64_t seed, const uint8_t *keep, int32_t *tn,
+                                                 int32_t *fgtot, float4 *pex, float4 *pix, uint32_t *exotic,
+                                                 int64_t nchv) {
+    constexpr int K = kCompactChunk / 256;
     const int b = blockIdx.y, blk = blockIdx.x;
-    const int fgb = fg[b];
     const int64_t P = (int64_t)H * W;
+    __shared__ int sh[8];
+    __shared__ int wcnt[K][4];
+    int2 tot = image_totals(blkcnt + b * nblk, nblk, blk, sh);
+    const int fgb = tot.x;
     if (fgb < min_num) {
-        if (blk == 0 && threadIdx.x == 0) tn[b] = 0;
+        if (blk == 0 && threadIdx.x == 0) { tn[b] = 0; fgtot[b] = fgb; }
         return;
     }
     const bool ds = fgb > max_num;
-    const int32_t *cnt = ds ? dscnt : blkcnt;
-    __shared__ int sh[8];
-    // exclusive prefix over the preceding blocks of this image
-    int pre = 0;
-    for (int j = threadIdx.x; j < blk; j += 256) pre += cnt[b * nblk + j];
-    pre = wave_sum_i(pre);
-    if (lane_id() == 0) sh[threadIdx.x / 64] = pre;
-    __syncthreads();
-    int base = sh[0] + sh[1] + sh[2] + sh[3];
-    if (blk == 0 && threadIdx.x == 0) tn[b] = ds ? tnds[b] : fgb;
+    int base = tot.y;
+    if (ds) {
+        int2 d = image_totals(dscnt + b * nblk, nblk, blk, sh);
+        base = d.y;
+        if (blk == 0 && threadIdx.x == 0) { tn[b] = d.x; fgtot[b] = fgb; }
+    } else if (blk == 0 && threadIdx.x == 0) {
+        tn[b] = fgb;
+        fgtot[b] = fgb;
+    }
     const float thr = ds ? (float)max_num / (float)fgb : 0.f;
-    const int wid = threadIdx.x / 64, lane = lane_id();
-    float2 *cb = coords + b * P;
-    float2 *rb = raw + (int64_t)b * vn * P;
-    for (int k = 0; k < kCompactChunk / 256; ++k) {
+    const int wid = threadIdx.x / 64;
+    bool f[K];
+    int below[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
         int64_t p = (int64_t)blk * kCompactChunk + k * 256 + threadIdx.x;
-        int r = (int)(p / W), c = (int)(p % W);
-        bool f = false;
-        if (p < P) {
-            f = is_fg<KIND, EVD>(m, b, r, c);
-            if (f && ds) f = keep ? keep[b * P + p] != 0 : rand_unit(seed, (uint64_t)b * P + p) < thr;
-        }
-        uint64_t bal = ballot(f);
-        int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-        __syncthreads();   // previous iteration finished reading sh[4..7]
-        if (lane == 0) sh[4 + wid] = __popcll(bal);
-        __syncthreads();
-        int woff = 0;
-        for (int q = 0; q < wid; ++q) woff += sh[4 + q];
-        int tot = sh[4] + sh[5] + sh[6] + sh[7];
-        if (f) {
-            int64_t t = base + woff + below;
-            cb[t] = make_float2((float)c, (float)r);
+        f[k] = p < P && is_fg<KIND, EVD>(m, b, (int)(p / W), (int)(p % W));
+        if (ds && f[k]) f[k] = keep ? keep[b * P + p] != 0 : rand_unit(seed, (uint64_t)b * P + p) < thr;
+        uint64_t bal = ballot(f[k]);
+        below[k] = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+        if (lane_id() == 0) wcnt[k][wid] = __popcll(bal);
+    }
+    __syncthreads();
+    float4 *eb = pex + (int64_t)b * vn * P;
+    float4 *pb = pix + (int64_t)b * vn * P;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        int off = base;
+        for (int q = 0; q < k; ++q) off += wcnt[q][0] + wcnt[q][1] + wcnt[q][2] + wcnt[q][3];
+        for (int q = 0; q < wid; ++q) off += wcnt[k][q];
+        if (f[k]) {
+            int64_t p = (int64_t)blk * kCompactChunk + k * 256 + threadIdx.x;
+            int r = (int)(p / W), c = (int)(p % W);
+            int64_t t = off + below[k];
             int64_t vo = b * vx.s[0] + r * vx.s[1] + c * vx.s[2];
+            bool exo = false;
+#pragma unroll 3
             for (int v = 0; v < vn; ++v) {
-                float a0, a1;
+                float nx, ny;
                 if (vx.kind == PV_VERTEX_F32) {
-                    const float *q = (const float *)vx.p;
-                    a0 = q[vo + v * vx.s[3]];
-                    a1 = q[vo + v * vx.s[3] + vx.s[4]];
+                    const float *q = (const float *)vx.p + vo;
+                    nx = q[v * vx.s[3]];
+                    ny = q[v * vx.s[3] + vx.s[4]];
                 } else {
-                    const __half *q = (const __half *)vx.p;
-                    a0 = __half2float(q[vo + v * vx.s[3]]);
-                    a1 = __half2float(q[vo + v * vx.s[3] + vx.s[4]]);
+                    const __half *q = (const __half *)vx.p + vo;
+                    nx = __half2float(q[v * vx.s[3]]);
+                    ny = __half2float(q[v * vx.s[3] + vx.s[4]]);
                 }
-                rb[(int64_t)v * P + t] = make_float2(a0, a1);
+                eb[(int64_t)v * P + t] = make_float4((float)c, (float)r, nx, ny);
+                // fast-test data: exact norm1 validity (KU:119-121), unit direction via fp64
+                float n1 = sqrtf(nx * nx + ny * ny);
+                bool valid = !((double)n1 < 1e-6);
+                exo |= valid && !(n1 <= kN1Max);
+                double N = sqrt((double)nx * nx + (double)ny * ny);
+                pb[(int64_t)v * P + t] = make_float4(valid ? (float)c : __builtin_nanf(""), (float)r,
+                                                     (float)(nx / N), (float)(ny / N));
+            }
+            if (exo) atomicOr(&exotic[b * nchv + t / kVoteChunk], 1u);
+        }
+    }
+}
+
+// ==========================================================================
+// K4: hypotheses (KU:11-49) + fused vote/count.
+// counts[b][v][h] += #{t : inlier(h, v, t)}.
+//
+// Work item = (image, keypoint v, chunk of 256 pixels, group of 64
+// hypotheses); one item per wave, items strided over a fixed grid.  Lane =
+// hypothesis: each wave generates its own 64 hypotheses (pixel pairs from the
+// caller or the counter RNG, RV:553) and the chunk-0 wave of each group stores
+// them for the refine stage.  The pixels are wave-uniform and come through
+// scalar loads, so a pixel costs no vector instruction besides the test, and
+// the per-lane inlier count is one v_addc on the compare's VCC.
+//
+// The test (fast path) works in the pixel's rotated frame: with u the unit
+// predicted direction and d = h - c,
+//     x' = u.d,  y' = u x d,    cos(u,d) > thr  <=>  x' tau - |y'| > 0,
+//     tau = sqrt(1 - thr^2) / thr   (0 < thr < 1),
+// i.e. 2 subs + 4 mul/fma + 1 fma + compare: no sqrt, rsq or division.
+// A pair is decided by the fast path only when |z| = |x' tau - |y'|| exceeds
+// gz * D, where D >= |d| bounds the distance to every pixel of the chunk and
+// gz covers both the fast path's rounding and the reference's own (<= 8 ulp
+// on the cosine, KU:119-123); the rest (and hypotheses / pixels outside the
+// bound's domain) are re-decided with the reference's exact sequence.  See
+// DESIGN.md "Exactness of the fast vote test" for the derivation.
+// ==========================================================================
+// plain PODs read through the constant address space -> s_load (scalar) loads
+struct alignas(16) F4 { float x, y, z, w; };
+struct alignas(8) F2 { float x, y; };
+// a pointer the compiler can see is wave-uniform (so loads through it become s_load)
+template <typename T>
+__device__ __forceinline__ T *uptr(T *p) {
+    uint64_t v = (uint64_t)p;
+    uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (T *)(((uint64_t)hi << 32) | lo);
+}
+
+struct VoteArgs {
+    const float4 *pix;          // PREPPED: fast data (fx, cy, ux, uy): pix[(b*vn + v)*P + t]
+    const float4 *pex;          // PREPPED: exact data (cx, cy, nx, ny), same layout
+    const uint32_t *exotic;     // PREPPED: 256-pixel chunk holds a pixel outside the fast domain
+    const float2 *coords;       // !PREPPED: coords[b*P + t]
+    const float2 *raw;          // !PREPPED: raw[b*vn*P + v*raw_v + t*raw_t]
+    const float2 *hyp;          // !GEN: hyp[(b*nh + h)*vn + v]
+    float2 *hyp_out;            // GEN: generated hypotheses, same layout
+    float *diag_hyp;            // GEN: optional copy [b][nh][vn][2]
+    const int32_t *idxs;        // GEN: pixel pairs [b][nh][vn][2], or nullptr (counter RNG)
+    int32_t *counts;            // counts[b*cnt_bs + v*cnt_v + h*cnt_h]
+    const int32_t *tn_dev;      // [b] pixels per image, or nullptr (tn_host)
+    uint64_t seed;
+    int32_t P, raw_v, raw_t, exotic_b, cnt_v, cnt_h, cnt_bs;
+    int32_t tn_host, b, vn, nh, hgn, fast;
+    float thr, tau, gzf, gzr;
+};
+
+// the reference's operands of pixel t: (cx, cy, nx, ny)
+template <bool PREPPED>
+__device__ __forceinline__ F4 pixel_exact(const VoteArgs &a, int b, int v, int t) {
+    if (PREPPED) {
+        const float4 e = a.pex[((int64_t)b * a.vn + v) * a.P + t];
+        return F4{e.x, e.y, e.z, e.w};
+    }
+    const float2 c = a.coords[(int64_t)b * a.P + t];
+    const float2 d = a.raw[(int64_t)b * a.vn * a.P + (int64_t)v * a.raw_v + (int64_t)t * a.raw_t];
+    return F4{c.x, c.y, d.x, d.y};
+}
+
+// the hypothesis of lane h (exact value; (0, 0) for a degenerate pair, KU:33-41)
+template <bool GEN, bool PREPPED>
+__device__ __forceinline__ float2 item_hyp(const VoteArgs &a, int b, int v, int h, bool hl, int n, bool store) {
+    float x = 0.f, y = 0.f;
+    if (GEN) {
+        if (hl) {
+            int64_t gid = ((int64_t)b * a.nh + h) * a.vn + v;
+            int t0, t1;
+            if (a.idxs) {
+                t0 = min(max(a.idxs[gid * 2], 0), n - 1);
+                t1 = min(max(a.idxs[gid * 2 + 1], 0), n - 1);
+            } else {
+                t0 = rand_index(a.seed, (uint64_t)gid * 2, n);
+                t1 = rand_index(a.seed, (uint64_t)gid * 2 + 1, n);
+            }
+            const F4 e0 = pixel_exact<PREPPED>(a, b, v, t0), e1 = pixel_exact<PREPPED>(a, b, v, t1);
+            float ox, oy;
+            if (exact_intersect(e0.z, e0.w, e0.x, e0.y, e1.z, e1.w, e1.x, e1.y, &ox, &oy)) { x = ox; y = oy; }
+            if (store) {
+                a.hyp_out[gid] = make_float2(x, y);
+                if (a.diag_hyp) { a.diag_hyp[gid * 2] = x; a.diag_hyp[gid * 2 + 1] = y; }
             }
         }
-        base += tot;
+    } else if (hl) {
+        float2 q = a.hyp[((int64_t)b * a.nh + h) * a.vn + v];
+        x = q.x; y = q.y;
     }
+    return make_float2(x, y);
 }
-
-// ==========================================================================
-// K3: hypotheses (KU:11-49) for every (image, h, v); pixel pairs from the
-// caller (parity) or from the counter RNG (RV:553 random_(0, tn)).
-// ==========================================================================
-__global__ __launch_bounds__(256) void k_generate(const float2 *coords, const float2 *raw, const int32_t *tn,
-                                                  int64_t P, int b_n, int vn, int nh, const int32_t *idxs_in,
-                                                  uint64_t seed, float2 *hyp, float2 *hypf, int32_t *item_base,
-                                                  int hgn, float *diag_hyp) {
-    int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (gid == 0) {   // vote-item prefix for the count kernel
-        int acc = 0;
-        for (int b = 0; b < b_n; ++b) {
-            item_base[b] = acc;
-            int nch = (tn[b] + kVoteChunk - 1) / kVoteChunk;
-            acc += vn * hgn * nch;
-        }
-        item_base[b_n] = acc;
-    }
-    if (gid >= (int64_t)b_n * nh * vn) return;
-    int v = (int)(gid % vn);
-    int h = (int)((gid / vn) % nh);
-    int b = (int)(gid / ((int64_t)vn * nh));
-    int n = tn[b];
-    float x = 0.f, y = 0.f;
-    if (n > 0) {
-        int t0, t1;
-        if (idxs_in) {
-            t0 = idxs_in[gid * 2];
-            t1 = idxs_in[gid * 2 + 1];
-            t0 = min(max(t0, 0), n - 1);
-            t1 = min(max(t1, 0), n - 1);
-        } else {
-            t0 = rand_index(seed, (uint64_t)gid * 2, n);
-            t1 = rand_index(seed, (uint64_t)gid * 2 + 1, n);
-        }
-        const float2 *rv = raw + ((int64_t)b * vn + v) * P;
-        const float2 *cb = coords + (int64_t)b * P;
-        float2 d0 = rv[t0], d1 = rv[t1], c0 = cb[t0], c1 = cb[t1];
-        float ox, oy;
-        if (exact_intersect(d0.x, d0.y, c0.x, c0.y, d1.x, d1.y, c1.x, c1.y, &ox, &oy)) { x = ox; y = oy; }
-    }
-    hyp[gid] = make_float2(x, y);
-    if (diag_hyp) { diag_hyp[gid * 2] = x; diag_hyp[gid * 2 + 1] = y; }
-    float nan = __builtin_nanf("");
-    bool ex = hyp_exact_only(x, y);
-    hypf[((int64_t)b * vn + v) * nh + h] = ex ? make_float2(nan, nan) : make_float2(x, y);
-}
-
-// ==========================================================================
-// K4: fused vote + count.  counts[b][v][h] += #{t : inlier(h, v, t)}.
-// Work item = (image, keypoint v, hypothesis group of 128, chunk of 256
-// pixels); one item per wave, items strided over a fixed grid.
-// ==========================================================================
-struct VoteArgs {
-    const float2 *coords; int64_t coords_b;           // coords(b,t) = coords[b*coords_b + t]
-    const float2 *raw; int64_t raw_b, raw_v, raw_t;   // raw(b,v,t)
-    const float2 *hypf;                               // [b][vn][nh] fast copy (or nullptr -> derive from hyp)
-    const float2 *hyp; int64_t hyp_b;                 // hyp(b,h,v) = hyp[b*hyp_b + h*vn + v]
-    int32_t *counts; int64_t cnt_b, cnt_v, cnt_h;     // counts(b,v,h) = counts[b*cnt_b + v*cnt_v + h*cnt_h]
-    const int32_t *tn_dev; int tn_host;
-    const int32_t *item_base;                         // [b+1] or nullptr (single image, host tn)
-    int b, vn, nh, hgn;
-    float thr, thr_hi, thr_lo;
-};
 
 __device__ __forceinline__ float bcast(float x, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), lane));
 }
 
-// v_writelane: put the wave-uniform `val` into lane `lane` of `dst` (1 VALU).
-// gfx950 allows one SGPR on the constant bus, so the lane select goes through
-// M0 (which no other instruction of these kernels uses: checked in the .s).
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-__device__ __forceinline__ int write_lane(int dst, int val, int lane) {
-    val = __builtin_amdgcn_readfirstlane(val);
-    lane = __builtin_amdgcn_readfirstlane(lane);
-    asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(dst) : "s"(val), "s"(lane) : "m0");
-    return dst;
+__device__ __forceinline__ float wave_min(float x) {
+    for (int o = 32; o > 0; o >>= 1) x = fminf(x, __shfl_xor(x, o));
+    return x;
 }
-#pragma clang diagnostic pop
+__device__ __forceinline__ float wave_max(float x) {
+    for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
+    return x;
+}
 
-template <bool PARTIAL, bool PREPPED>
-__device__ __forceinline__ void vote_item(const VoteArgs &a, int b, int v, int hg, int chunk, int n) {
+// fast data of one pixel from its raw direction (API path without a prepped array)
+__device__ __forceinline__ float4 prep_pixel(float cx, float cy, float nx, float ny) {
+    float n1 = sqrtf(nx * nx + ny * ny);                 // exactly the reference's norm1
+    bool ok = !((double)n1 < 1e-6);
+    double N = sqrt((double)nx * nx + (double)ny * ny);
+    return make_float4(ok ? cx : __builtin_nanf(""), cy, (float)(nx / N), (float)(ny / N));
+}
+
+__device__ __forceinline__ bool pixel_exotic(float nx, float ny) {
+    float n1 = sqrtf(nx * nx + ny * ny);
+    return !((double)n1 < 1e-6) && !(n1 <= kN1Max);     // votes, but outside the fast domain
+}
+
+// One segment = pixels [ts, te) of one (image b, keypoint v, hypothesis group
+// hg) against the group's kGroup hypotheses (kHypLane per lane).
+//
+// Pixels are staged per sub-chunk of 256 in two LDS slabs of the wave: the
+// fast operands (ux, uy, -k1, -k2) with k1 = u.c', k2 = u x c' and c' = c - o
+// relative to the sub-chunk origin o (an integer corner of its bounding box,
+// so c' is exact for pixel centres), and the reference's operands (cx, cy,
+// nx, ny) for the rare exact decisions.  For h' = h - o:
+//     x' = u.h' - k1,  y' = u x h' - k2,  z = x' tau - |y'|
+// = 4 fma + 1 fma, a compare for the count and a min for the guard band.
+// The band is gzf * B + gzr * D: B >= |h'| + |c'| bounds the fast path's own
+// rounding (per sub-chunk), D >= |h - c| the reference's (per 64-pixel
+// quarter, from the quarter's bounding box).
+constexpr int kHypLane = 2;
+constexpr int kGroup = kWave * kHypLane;
+
+template <bool GEN, bool PREPPED>
+__device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, F4 *stagex, int b, int v, int hg, int ts,
+                                             int te, int n) {
     const int lane = lane_id();
-    Pix px[kVotePix];
-    uint64_t vmask[kVotePix];
-    const float2 *cb = a.coords + b * a.coords_b;
-    const float2 *rb = a.raw + b * a.raw_b + v * a.raw_v;
+    const float tau = a.tau;
+    constexpr float kBig = 3.0e38f;
+
+    float2 he[kHypLane];     // exact hypotheses (the reference's operands)
+    bool hf[kHypLane];       // decided by the fast test
+    bool hxo[kHypLane];      // outside the fast test's domain: exact only
+    int cnt[kHypLane];
 #pragma unroll
-    for (int p = 0; p < kVotePix; ++p) {
-        int t = chunk * kVoteChunk + p * kWave + lane;
-        bool in = t < n;
-        int tt = in ? t : 0;
-        float2 c = cb[tt];
-        float2 d = rb[(int64_t)tt * a.raw_t];
-        if (!in) { d = make_float2(0.f, 0.f); }
-        px[p] = make_pix(c.x, c.y, d.x, d.y);
-        vmask[p] = PARTIAL ? ballot(in) : ~0ull;
+    for (int i = 0; i < kHypLane; ++i) {
+        const int h = hg * kGroup + i * kWave + lane;
+        const bool hl = h < a.nh;
+        he[i] = item_hyp<GEN, PREPPED>(a, b, v, h, hl, n, ts == 0);
+        const bool fin = isfinite(he[i].x) && isfinite(he[i].y);    // non-finite: never an inlier
+        hxo[i] = hl && fin && hyp_exact_only(he[i].x, he[i].y);
+        hf[i] = hl && fin && !hxo[i];
+        cnt[i] = 0;
     }
-    const int h0 = hg * kVoteHG;
-    const int h1 = min(h0 + kVoteHG, a.nh);
-    const float2 *hf = PREPPED ? a.hypf + ((int64_t)b * a.vn + v) * a.nh : nullptr;
-    const float2 *he = a.hyp + b * a.hyp_b + v;
-    int32_t *cnt = a.counts + b * a.cnt_b + v * a.cnt_v;
-    for (int hb = h0; hb < h1; hb += kWave) {
-        const int hn_blk = uniform(min(kWave, h1 - hb));
-        // this block's 64 hypotheses: one per lane, broadcast with v_readlane in the loop
-        const bool hl = lane < hn_blk;
-        float2 qe = hl ? he[(int64_t)(hb + lane) * a.vn] : make_float2(0.f, 0.f);
-        float2 qf;
-        if (PREPPED) {
-            qf = hl ? hf[hb + lane] : make_float2(0.f, 0.f);
-        } else {
-            bool ex = hyp_exact_only(qe.x, qe.y);
-            qf = ex ? make_float2(__builtin_nanf(""), __builtin_nanf("")) : qe;
-        }
-        int my = 0;
-        for (int hh = 0; hh < hn_blk; ++hh) {
-            const float hx = bcast(qf.x, hh), hy = bcast(qf.y, hh);
-            int c = 0;
-            uint64_t unc_any = 0;
-            uint64_t unc[kVotePix];
+
+    for (int s0 = ts; s0 < te; s0 += kVoteChunk) {
+        const int np = min(kVoteChunk, te - s0);
+        F4 q4[kVoteChunk / kWave];
+        float xl[kVoteChunk / kWave], xh[kVoteChunk / kWave];
+        bool exo_p = false;
 #pragma unroll
-            for (int p = 0; p < kVotePix; ++p) {
-                float cs = fast_cos(px[p], hx, hy);
-                uint64_t mhi = ballot(cs > a.thr_hi);
-                uint64_t mmay = ballot(!(cs <= a.thr_lo));
-                if (PARTIAL) { mhi &= vmask[p]; mmay &= vmask[p]; }
-                c += __popcll(mhi);
-                unc[p] = mmay & ~mhi;
-                unc_any |= unc[p];
+        for (int k = 0; k < kVoteChunk / kWave; ++k) {
+            const int j = k * kWave + lane;
+            F4 q{__builtin_nanf(""), 0.f, 0.f, 0.f};
+            xl[k] = kBig;
+            xh[k] = -kBig;
+            if (j < np) {
+                const F4 e = pixel_exact<PREPPED>(a, b, v, s0 + j);
+                if (PREPPED) {
+                    const float4 f = a.pix[((int64_t)b * a.vn + v) * a.P + s0 + j];
+                    q = F4{f.x, f.y, f.z, f.w};
+                } else {
+                    const float4 f = prep_pixel(e.x, e.y, e.z, e.w);
+                    q = F4{f.x, f.y, f.z, f.w};
+                    exo_p |= pixel_exotic(e.z, e.w);
+                }
+                stagex[j] = e;
+                xl[k] = e.x;
+                xh[k] = e.x;
             }
-            if (unc_any) {   // rare: re-decide the guard band with the reference sequence
-                const float ex = bcast(qe.x, hh), ey = bcast(qe.y, hh);
+            q4[k] = q;
+        }
+        bool slow = !a.fast;
+        if (PREPPED) {
+            const uint32_t *ex = a.exotic + (int64_t)b * a.exotic_b;
+            slow |= (ex[s0 / kVoteChunk] | ex[(s0 + np - 1) / kVoteChunk]) != 0;
+        } else {
+            slow |= __builtin_amdgcn_ballot_w64(exo_p) != 0;
+        }
+        slow = __builtin_amdgcn_readfirstlane(slow);
+        // per-quarter bounding boxes (lane k of qxl..qyh holds quarter k); the
+        // compacted pixels are row-major, so a quarter's rows run from its
+        // first pixel to its last (the API path takes arbitrary coordinates)
+        float qxl = kBig, qxh = -kBig, qyl = kBig, qyh = -kBig;
+        float cxl = kBig, cxh = -kBig, cyl = kBig, cyh = -kBig;
 #pragma unroll
-                for (int p = 0; p < kVotePix; ++p) {
-                    if (unc[p]) {
-                        bool e = exact_vote(px[p].nx, px[p].ny, px[p].cx, px[p].cy, ex, ey, a.thr);
-                        c += __popcll(ballot(e) & unc[p]);
+        for (int k = 0; k < kVoteChunk / kWave; ++k) {
+            if (k * kWave < np) {
+                const float mn = wave_min(xl[k]), mx = wave_max(xh[k]);
+                float yn, yx;
+                if (PREPPED) {
+                    yn = bcast(q4[k].y, 0);
+                    yx = bcast(q4[k].y, min(kWave - 1, np - 1 - k * kWave));
+                } else {
+                    const bool in = k * kWave + lane < np;
+                    yn = wave_min(in ? q4[k].y : kBig);
+                    yx = wave_max(in ? q4[k].y : -kBig);
+                }
+                if (lane == k) { qxl = mn; qxh = mx; qyl = yn; qyh = yx; }
+                cxl = fminf(cxl, mn); cxh = fmaxf(cxh, mx);
+                cyl = fminf(cyl, yn); cyh = fmaxf(cyh, yx);
+            }
+        }
+        const bool empty = !(cxl <= cxh) || !(cyl <= cyh);
+        const float ox = empty ? 0.f : floorf(cxl), oy = empty ? 0.f : floorf(cyl);
+        const float R = empty ? 0.f
+                              : __builtin_amdgcn_sqrtf(fmaf(cxh - ox, cxh - ox, (cyh - oy) * (cyh - oy))) * 1.00001f;
+        // stage the fast operands (ux, uy, -k1, -k2)
+#pragma unroll
+        for (int k = 0; k < kVoteChunk / kWave; ++k) {
+            const F4 q = q4[k];
+            const float cx = q.x - ox, cy = q.y - oy;          // exact for pixel centres
+            const float k1 = fmaf(q.z, cx, q.w * cy);          // NaN for invalid pixels
+            const float k2 = fmaf(q.z, cy, -(q.w * cx));
+            stage[k * kWave + lane] = F4{q.z, q.w, -k1, -k2};
+        }
+        __builtin_amdgcn_wave_barrier();
+        // lane constants of this sub-chunk
+        float hx[kHypLane], hy[kHypLane], Bv[kHypLane], gd[kHypLane];
+#pragma unroll
+        for (int i = 0; i < kHypLane; ++i) {
+            hx[i] = hf[i] ? he[i].x - ox : __builtin_nanf("");
+            hy[i] = hf[i] ? he[i].y - oy : __builtin_nanf("");
+            Bv[i] = (__builtin_amdgcn_sqrtf(fmaf(hx[i], hx[i], hy[i] * hy[i])) + R) * 1.00001f + 1e-30f;
+            gd[i] = 0.f;
+        }
+        // band of quarter k
+        auto set_band = [&](int k) {
+            const float xn = bcast(qxl, k) - ox, xx = bcast(qxh, k) - ox;
+            const float yn = bcast(qyl, k) - oy, yx = bcast(qyh, k) - oy;
+#pragma unroll
+            for (int i = 0; i < kHypLane; ++i) {
+                const float ax = fmaxf(fabsf(hx[i] - xn), fabsf(hx[i] - xx));
+                const float ay = fmaxf(fabsf(hy[i] - yn), fabsf(hy[i] - yx));
+                const float D = fmaf(__builtin_amdgcn_sqrtf(fmaf(ax, ax, ay * ay)), 1.00001f, Bv[i] * 1e-6f);
+                const float g = fmaf(a.gzr, D, a.gzf * Bv[i]);
+                gd[i] = g >= 0.f ? g : __builtin_inff();
+            }
+        };
+        if (!slow) {
+            auto zval = [&](const F4 &q, float hxi, float hyi) {
+                const float xr = fmaf(q.x, hxi, fmaf(q.y, hyi, q.z));      // u.h' - k1
+                const float yr = fmaf(q.x, hyi, fmaf(-q.y, hxi, q.w));     // u x h' - k2
+                return fmaf(xr, tau, -fabsf(yr));
+            };
+            // rare: some pair of pixels [j, j+4) is inside the band.  One (pixel,
+            // hypothesis) pair per iteration, not unrolled, so the hot loop's
+            // registers stay free; the exact operands come from the LDS slab.
+            auto fix_step = [&](int j) {
+#pragma unroll 1
+                for (int pi = 0; pi < 4 * kHypLane; ++pi) {
+                    const int p = pi >> 1;
+                    const bool i1 = pi & 1;
+                    const float hxi = i1 ? hx[1] : hx[0], hyi = i1 ? hy[1] : hy[0], gdi = i1 ? gd[1] : gd[0];
+                    const bool u = fabsf(zval(stage[j + p], hxi, hyi)) <= gdi;
+                    if (__builtin_amdgcn_ballot_w64(u)) {
+                        const F4 e = stagex[j + p];
+                        const float ex = i1 ? he[1].x : he[0].x, ey = i1 ? he[1].y : he[0].y;
+                        const int r = (u && exact_vote(e.z, e.w, e.x, e.y, ex, ey, a.thr)) ? 1 : 0;
+                        cnt[0] += i1 ? 0 : r;
+                        cnt[1] += i1 ? r : 0;
                     }
                 }
+            };
+            // 4 pixels x 2 hypotheses per step, LDS reads one step ahead into
+            // two named buffers (no register copies).  The band is checked once
+            // per step on min |z| (v_min ignores NaN, so invalid pixels and
+            // non-fast hypotheses never trigger it).
+            auto step = [&](F4 q0, F4 q1, F4 q2, F4 q3, int j) {
+                float m0 = kBig, m1 = kBig;
+                float z;
+                z = zval(q0, hx[0], hy[0]); cnt[0] += z > gd[0]; m0 = fminf(m0, fabsf(z));
+                z = zval(q0, hx[1], hy[1]); cnt[1] += z > gd[1]; m1 = fminf(m1, fabsf(z));
+                z = zval(q1, hx[0], hy[0]); cnt[0] += z > gd[0]; m0 = fminf(m0, fabsf(z));
+                z = zval(q1, hx[1], hy[1]); cnt[1] += z > gd[1]; m1 = fminf(m1, fabsf(z));
+                z = zval(q2, hx[0], hy[0]); cnt[0] += z > gd[0]; m0 = fminf(m0, fabsf(z));
+                z = zval(q2, hx[1], hy[1]); cnt[1] += z > gd[1]; m1 = fminf(m1, fabsf(z));
+                z = zval(q3, hx[0], hy[0]); cnt[0] += z > gd[0]; m0 = fminf(m0, fabsf(z));
+                z = zval(q3, hx[1], hy[1]); cnt[1] += z > gd[1]; m1 = fminf(m1, fabsf(z));
+                if (__builtin_amdgcn_ballot_w64(m0 <= gd[0] || m1 <= gd[1])) fix_step(j);
+            };
+            static_assert(kHypLane == 2, "step() is written for two hypotheses per lane");
+            // the slab past np holds NaN pixels (never counted, never in the
+            // band), so the loop runs whole 8-pixel iterations
+            const int nit = (np + 7) >> 3;
+            F4 a0 = stage[0], a1 = stage[1], a2 = stage[2], a3 = stage[3];
+            for (int it = 0; it < nit; ++it) {
+                const int j = it * 8;
+                if ((j & (kWave - 1)) == 0) set_band(j / kWave);
+                const F4 b0 = stage[j + 4], b1 = stage[j + 5], b2 = stage[j + 6], b3 = stage[j + 7];
+                step(a0, a1, a2, a3, j);
+                const int jn = (j + 8) & (kVoteChunk - 1);
+                a0 = stage[jn]; a1 = stage[jn + 1]; a2 = stage[jn + 2]; a3 = stage[jn + 3];
+                step(b0, b1, b2, b3, j + 4);
             }
-            my = write_lane(my, c, hh);
+            // exact-only hypotheses (rare): lane = pixel, one hypothesis at a time
+#pragma unroll
+            for (int i = 0; i < kHypLane; ++i) {
+                uint64_t m = __builtin_amdgcn_ballot_w64(hxo[i]);
+                while (m) {
+                    const int l = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const float ex = bcast(he[i].x, l), ey = bcast(he[i].y, l);
+                    int c = 0;
+#pragma unroll
+                    for (int k = 0; k < kVoteChunk / kWave; ++k) {
+                        const int jj = k * kWave + lane;
+                        bool e = false;
+                        if (jj < np) {
+                            const F4 x = stagex[jj];
+                            e = exact_vote(x.z, x.w, x.x, x.y, ex, ey, a.thr);
+                        }
+                        c += __popcll(__builtin_amdgcn_ballot_w64(e));
+                    }
+                    if (lane == l) cnt[i] += c;
+                }
+            }
+        } else {
+            // every pair through the reference sequence
+#pragma unroll 1
+            for (int j = 0; j < np; ++j) {
+                const F4 e = stagex[j];
+#pragma unroll
+                for (int i = 0; i < kHypLane; ++i) cnt[i] += exact_vote(e.z, e.w, e.x, e.y, he[i].x, he[i].y, a.thr);
+            }
         }
-        if (hl && my) atomicAdd(&cnt[(int64_t)(hb + lane) * a.cnt_h], my);
+        __builtin_amdgcn_wave_barrier();
+    }
+    int32_t *cp = a.counts + (int64_t)b * a.cnt_bs + (int64_t)v * a.cnt_v;
+#pragma unroll
+    for (int i = 0; i < kHypLane; ++i) {
+        const int h = hg * kGroup + i * kWave + lane;
+        if (h < a.nh && cnt[i]) atomicAdd(&cp[(int64_t)h * a.cnt_h], cnt[i]);
     }
 }
 
-template <bool PREPPED>
-__device__ __forceinline__ void vote_item_any(const VoteArgs &a, int b, int v, int hg, int chunk, int n) {
-    if ((chunk + 1) * kVoteChunk <= n) vote_item<false, PREPPED>(a, b, v, hg, chunk, n);
-    else vote_item<true, PREPPED>(a, b, v, hg, chunk, n);
-}
-
+// Balanced persistent waves: the (image, keypoint, hypothesis group, pixel)
+// work space is linearised with pixels fastest and cut into equal contiguous
+// ranges, one per wave, so every wave does the same number of pixel steps and
+// generates each group's hypotheses once per range.
+template <bool GEN, bool PREPPED>
 __global__ __launch_bounds__(256) void k_vote_count(VoteArgs a) {
     const int wave = uniform((int)(blockIdx.x * 4 + threadIdx.x / 64));
-    const int nwaves = gridDim.x * 4;
-    int total;
-    if (a.item_base) total = a.item_base[a.b];
-    else total = a.vn * a.hgn * ((a.tn_host + kVoteChunk - 1) / kVoteChunk);
-    for (int item = wave; item < total; item += nwaves) {
-        int b = 0;
-        if (a.item_base) {
-            while (a.item_base[b + 1] <= item) ++b;
-        }
+    const int64_t nwaves = (int64_t)gridDim.x * 4;
+    __shared__ F4 stage_all[4][kVoteChunk];
+    __shared__ F4 stagex_all[4][kVoteChunk];
+    F4 *stage = stage_all[threadIdx.x / 64];
+    F4 *stagex = stagex_all[threadIdx.x / 64];
+    int64_t total = 0;
+    for (int b = 0; b < a.b; ++b) total += (int64_t)a.vn * a.hgn * (a.tn_dev ? a.tn_dev[b] : a.tn_host);
+    int64_t lo = total * wave / nwaves, hi = total * (wave + 1) / nwaves;
+    // walk the segments of [lo, hi)
+    int b = 0;
+    int64_t base = 0;
+    while (lo < hi) {
         int n = a.tn_dev ? a.tn_dev[b] : a.tn_host;
-        int nch = (n + kVoteChunk - 1) / kVoteChunk;
-        int r = item - (a.item_base ? a.item_base[b] : 0);
-        int hg = r % a.hgn;
-        r /= a.hgn;
-        int chunk = r % nch;
-        int v = r / nch;
-        b = uniform(b); hg = uniform(hg); chunk = uniform(chunk); v = uniform(v); n = uniform(n);
-        if (a.hypf) vote_item_any<true>(a, b, v, hg, chunk, n);
-        else vote_item_any<false>(a, b, v, hg, chunk, n);
-    }
-}
-
-// ==========================================================================
-// K6: winner per (image, keypoint) (RV:567-575) + least-squares partial sums
-// over the winner's inliers (RV:584-599), accumulated in fp64.
-// ==========================================================================
-__global__ __launch_bounds__(256) void k_refine(const int32_t *counts, const float2 *hyp, const float2 *coords,
-                                                const float2 *raw, const int32_t *tn, int64_t P, int vn, int nh,
-                                                float thr, int32_t *win_out, float *ratio_out, float2 *best_out,
-                                                double *refpart) {
-    const int j = blockIdx.x, v = blockIdx.y, b = blockIdx.z;
-    const int n = tn[b];
-    __shared__ uint64_t skey[4];
-    __shared__ double sacc[4][5];
-    // argmax over h, first index on ties: key = count << 32 | ~h
-    uint64_t key = 0;
-    const int32_t *cnt = counts + ((int64_t)b * vn + v) * nh;
-    for (int h = threadIdx.x; h < nh; h += 256) {
-        uint64_t k2 = ((uint64_t)(uint32_t)cnt[h] << 32) | (uint32_t)(0xffffffffu - (uint32_t)h);
-        key = k2 > key ? k2 : key;
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-        uint64_t other = __shfl_xor(key, o);
-        key = other > key ? other : key;
-    }
-    if (lane_id() == 0) skey[threadIdx.x / 64] = key;
-    __syncthreads();
-    key = skey[0];
-    for (int q = 1; q < 4; ++q) key = skey[q] > key ? skey[q] : key;
-    const int win = (int)(0xffffffffu - (uint32_t)key);
-    const int wcnt = (int)(key >> 32);
-    // RV:570-575: ratio = count / tn; best starts at 0 and is replaced only on a strict increase
-    const float ratio = n > 0 ? (float)wcnt / (float)n : 0.f;
-    float2 best = make_float2(0.f, 0.f);
-    if (n > 0 && 0.f < ratio) best = hyp[((int64_t)b * nh + win) * vn + v];
-    if (j == 0 && threadIdx.x == 0) {
-        int o = b * vn + v;
-        win_out[o] = n > 0 ? win : 0;
-        ratio_out[o] = ratio;
-        best_out[o] = best;
-    }
-    double acc[5] = {0, 0, 0, 0, 0};
-    const float2 *cb = coords + (int64_t)b * P;
-    const float2 *rv = raw + ((int64_t)b * vn + v) * P;
-    for (int t = j * 256 + threadIdx.x; t < n; t += kRefineNJ * 256) {
-        float2 c = cb[t], d = rv[t];
-        if (exact_vote(d.x, d.y, c.x, c.y, best.x, best.y, thr)) {
-            float n0 = d.y, n1 = -d.x;                  // RV:585-587 normal = (d_y, -d_x)
-            float bb = n0 * c.x + n1 * c.y;             // RV:597 (2-term fp32 sum)
-            acc[0] += (double)n0 * n0;
-            acc[1] += (double)n0 * n1;
-            acc[2] += (double)n1 * n1;
-            acc[3] += (double)n0 * bb;
-            acc[4] += (double)n1 * bb;
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        double s = wave_sum_d(acc[k]);
-        if (lane_id() == 0) sacc[threadIdx.x / 64][k] = s;
-    }
-    __syncthreads();
-    if (threadIdx.x < 5) {
-        int k = threadIdx.x;
-        double s = sacc[0][k] + sacc[1][k] + sacc[2][k] + sacc[3][k];
-        refpart[(((int64_t)b * vn + v) * kRefineNJ + j) * 5 + k] = s;
+        int64_t span = (int64_t)a.vn * a.hgn * n;
+        if (lo >= base + span) { base += span; ++b; continue; }
+        int64_t r = lo - base;
+        int g = (int)(r / n);               // (v, hg) group index
+        int ts = (int)(r - (int64_t)g * n);
+        int te = (int)min<int64_t>((int64_t)n, ts + (hi - lo));
+        int v = g / a.hgn, hg = g % a.hgn;
+        vote_segment<GEN, PREPPED>(a, stage, stagex, uniform(b), uniform(v), uniform(hg), uniform(ts), uniform(te),
+                                   n);
+        lo += te - ts;
     }
 }
 
@@ -649,45 +820,122 @@ __device__ inline bool lu2_inv(float a00, float a01, float a10, float a11, float
     return true;
 }
 
-// K7: per image: reduce the partial sums, b_inv with its batch-wide identity
-// fallback (RV:503-518), pts = b_inv(ATA) @ ATb (RV:600); iteration count of
-// the reference's loop for diagnostics (RV:578-582).
-__global__ __launch_bounds__(64) void k_solve(const double *refpart, const float *ratio, const int32_t *tn, int vn,
-                                              int nh, float confidence, int max_iter, float *out, pv_v3_diag diag,
-                                              const int32_t *win) {
-    const int b = blockIdx.x, v = threadIdx.x;
+template <typename T>
+__device__ __forceinline__ void st_agent(T *p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// ==========================================================================
+// K6: winner per (image, keypoint) (RV:567-575) + least-squares partial sums
+// over the winner's inliers (RV:584-599, fp64), then -- in the last block of
+// each image to finish -- b_inv with its batch-wide identity fallback
+// (RV:503-518) and pts = b_inv(ATA) @ ATb (RV:600).
+// Hand-off: partials stored write-through (sc1) and drained, one agent-scope
+// ticket add per block; the last block's wave 0 reads them with sc1 loads
+// (MI355X_MICROARCH.md "Valid forms", row 1).
+// ==========================================================================
+__global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, const float2 *hyp, const float4 *pex,
+                                                      const int32_t *tn, int64_t P, int vn, int nh,
+                                                      float thr, int32_t *win_out, float *ratio_out, double *refpart,
+                                                      int32_t *ticket, float confidence, int max_iter, float *out,
+                                                      pv_v3_diag diag) {
+    const int j = blockIdx.x, v = blockIdx.y, b = blockIdx.z;
     const int n = tn[b];
-    const bool act = v < vn;
-    float A00 = 0, A01 = 0, A11 = 0, B0 = 0, B1 = 0;
+    __shared__ uint64_t skey[4];
+    __shared__ double sacc[4][5];
+    __shared__ int slast;
+    // argmax over h, first index on ties: key = count << 32 | ~h
+    uint64_t key = 0;
+    const int32_t *cnt = counts + ((int64_t)b * vn + v) * nh;
+    for (int h = threadIdx.x; h < nh; h += 256) {
+        uint64_t k2 = ((uint64_t)(uint32_t)cnt[h] << 32) | (uint32_t)(0xffffffffu - (uint32_t)h);
+        key = k2 > key ? k2 : key;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        uint64_t other = __shfl_xor(key, o);
+        key = other > key ? other : key;
+    }
+    if (lane_id() == 0) skey[threadIdx.x / 64] = key;
+    __syncthreads();
+    key = skey[0];
+    for (int q = 1; q < 4; ++q) key = skey[q] > key ? skey[q] : key;
+    const int win = (int)(0xffffffffu - (uint32_t)key);
+    const int wcnt = (int)(key >> 32);
+    // RV:570-575: ratio = count / tn; best starts at 0 and is replaced only on a strict increase
+    const float ratio = n > 0 ? (float)wcnt / (float)n : 0.f;
+    float2 best = make_float2(0.f, 0.f);
+    if (n > 0 && 0.f < ratio) best = hyp[((int64_t)b * nh + win) * vn + v];
+    double acc[5] = {0, 0, 0, 0, 0};
+    const float4 *eb = pex + ((int64_t)b * vn + v) * P;
+    for (int t = j * 256 + threadIdx.x; t < n; t += kRefineNJ * 256) {
+        const float4 e = eb[t];   // (cx, cy, nx, ny)
+        if (exact_vote(e.z, e.w, e.x, e.y, best.x, best.y, thr)) {
+            float n0 = e.w, n1 = -e.z;                  // RV:585-587 normal = (d_y, -d_x)
+            float bb = n0 * e.x + n1 * e.y;             // RV:597 (2-term fp32 sum)
+            acc[0] += (double)n0 * n0;
+            acc[1] += (double)n0 * n1;
+            acc[2] += (double)n1 * n1;
+            acc[3] += (double)n0 * bb;
+            acc[4] += (double)n1 * bb;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        double s = wave_sum_d(acc[k]);
+        if (lane_id() == 0) sacc[threadIdx.x / 64][k] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {   // wave 0: publish this block's partials, then take a ticket
+        const int k = threadIdx.x;
+        double *rp = refpart + (((int64_t)b * vn + v) * kRefineNJ + j) * 5;
+        if (k < 5) st_agent(&rp[k], sacc[0][k] + sacc[1][k] + sacc[2][k] + sacc[3][k]);
+        if (j == 0 && k == 0) {
+            st_agent(&win_out[b * vn + v], n > 0 ? win : 0);
+            st_agent(&ratio_out[b * vn + v], ratio);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int t = 0;
+        if (k == 0) t = __hip_atomic_fetch_add(&ticket[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = __shfl(t, 0);
+        if (k == 0) slast = (t == kRefineNJ * vn - 1);
+    }
+    __syncthreads();
+    if (!slast || threadIdx.x >= 64) return;
+    // ---- last block of image b: solve for every keypoint (lane = keypoint) ----
+    const int vv = threadIdx.x;
+    const bool act = vv < vn;
+    float A00 = 0, A01 = 0, A11 = 0, B0 = 0, B1 = 0, rat = 3.0e38f;
+    int wi = 0;
     if (act) {
         double s[5] = {0, 0, 0, 0, 0};
-        const double *rp = refpart + ((int64_t)b * vn + v) * kRefineNJ * 5;
-        for (int j = 0; j < kRefineNJ; ++j)
-            for (int k = 0; k < 5; ++k) s[k] += rp[j * 5 + k];
+        const double *rp = refpart + ((int64_t)b * vn + vv) * kRefineNJ * 5;
+        for (int jj = 0; jj < kRefineNJ; ++jj)
+            for (int k = 0; k < 5; ++k) s[k] += ld_agent(&rp[jj * 5 + k]);
         A00 = (float)s[0]; A01 = (float)s[1]; A11 = (float)s[2]; B0 = (float)s[3]; B1 = (float)s[4];
+        rat = ld_agent(&ratio_out[b * vn + vv]);
+        wi = ld_agent(&win_out[b * vn + vv]);
     }
     float inv[4] = {1.f, 0.f, 0.f, 1.f};
     bool ok = act ? lu2_inv(A00, A01, A01, A11, inv) : true;
-    bool all_ok = __all(ok);
-    if (!all_ok) { inv[0] = 1.f; inv[1] = 0.f; inv[2] = 0.f; inv[3] = 1.f; }
+    if (!__all(ok)) { inv[0] = 1.f; inv[1] = 0.f; inv[2] = 0.f; inv[3] = 1.f; }   // RV:514-517
     if (act) {
         float x = inv[0] * B0 + inv[1] * B1;
         float y = inv[2] * B0 + inv[3] * B1;
         if (n == 0) { x = 0.f; y = 0.f; }
-        out[((int64_t)b * vn + v) * 2] = x;
-        out[((int64_t)b * vn + v) * 2 + 1] = y;
+        out[((int64_t)b * vn + vv) * 2] = x;
+        out[((int64_t)b * vn + vv) * 2 + 1] = y;
         if (diag.ata) {
-            float *q = diag.ata + ((int64_t)b * vn + v) * 4;
+            float *q = diag.ata + ((int64_t)b * vn + vv) * 4;
             q[0] = A00; q[1] = A01; q[2] = A01; q[3] = A11;
         }
-        if (diag.atb) { diag.atb[((int64_t)b * vn + v) * 2] = B0; diag.atb[((int64_t)b * vn + v) * 2 + 1] = B1; }
-        if (diag.win_ratio) diag.win_ratio[b * vn + v] = ratio[b * vn + v];
-        if (diag.win_idx) diag.win_idx[b * vn + v] = win[b * vn + v];
+        if (diag.atb) { diag.atb[((int64_t)b * vn + vv) * 2] = B0; diag.atb[((int64_t)b * vn + vv) * 2 + 1] = B1; }
+        if (diag.win_ratio) diag.win_ratio[b * vn + vv] = n > 0 ? rat : 0.f;
+        if (diag.win_idx) diag.win_idx[b * vn + vv] = wi;
     }
-    // min ratio over keypoints -> iterations of `while True` (identical work each time)
-    float r = act ? ratio[b * vn + v] : 3.0e38f;
+    // min ratio over keypoints -> iterations the reference's `while True` would run
+    float r = rat;
     for (int o = 32; o > 0; o >>= 1) r = fminf(r, __shfl_xor(r, o));
-    if (v == 0) {
+    if (vv == 0) {
         if (diag.tn) diag.tn[b] = n;
         if (diag.iters) {
             int it = 0;
@@ -936,7 +1184,7 @@ __global__ __launch_bounds__(256) void k_vote_bytes(const float *direct, const f
         float nx = direct[(int64_t)tt * vn * 2 + v * 2], ny = direct[(int64_t)tt * vn * 2 + v * 2 + 1];
         if (!in) { nx = 0.f; ny = 0.f; }
         Pix px = make_pix(coords[tt * 2], coords[tt * 2 + 1], nx, ny);
-        int h0 = hg * kVoteHG, h1 = min(h0 + kVoteHG, hn);
+        int h0 = hg * kBytesHG, h1 = min(h0 + kBytesHG, hn);
         for (int h = h0; h < h1; ++h) {
             float ex_x = hypo[(h * vn + v) * 2], ex_y = hypo[(h * vn + v) * 2 + 1];
             bool exo = hyp_exact_only(ex_x, ex_y);
@@ -1030,10 +1278,49 @@ void thresholds(float thr, float *hi, float *lo) {
     *lo = thr - kGuard;
 }
 
+// Constants of the rotated-frame test (DESIGN.md "Exactness of the fast vote
+// test"): tau = sqrt(1-thr^2)/thr; band = gzf * B + gzr * D with
+// B >= |h - o| + |c - o| and D >= |h - c|:
+//   gzf = 2 * (9 tau + 8) * 2^-24   the fast path's rounding (7 tau + 6, plus
+//                                   2 (tau + 1) for a rounded c - o when the
+//                                   coordinates are not integers)
+//   gzr = 2 * 9.5 (tau + 1/tau) * 2^-24   the reference's 8-ulp cosine error
+//                                   (+1.5 ulp for its rounded d) mapped
+//                                   through dz/dcos = |d| (tau + 1/tau)
+// both with 2x margin.
+void fast_constants(float thr, VoteArgs *va) {
+    va->thr = thr;
+    const double t = (double)thr;
+    if (t >= 0.05 && t <= 0.999999) {
+        const double tau = sqrt(1.0 - t * t) / t;
+        const double u = 1.0 / 16777216.0;
+        va->tau = (float)tau;
+        va->gzf = (float)(2.0 * (9.0 * tau + 8.0) * u * 1.0001);
+        va->gzr = (float)(2.0 * 9.5 * (tau + 1.0 / tau) * u * 1.0001);
+        va->fast = 1;
+    } else {   // outside the derivation's range: every pair takes the exact sequence
+        va->tau = 0.f;
+        va->gzf = 0.f;
+        va->gzr = 0.f;
+        va->fast = 0;
+    }
+}
+
 int vote_grid(int64_t items) {
     // at most 8 waves per SIMD resident: 256 CUs x 32 waves = 8192 waves = 2048 blocks
     int64_t cap = (int64_t)cu_count() * 8;
     int64_t need = (items + 3) / 4;
+    return (int)(need < 1 ? 1 : (need < cap ? need : cap));
+}
+
+// persistent vote grid: every block resident at once (the occupancy limit of
+// the kernel: LDS slabs, registers), fewer when the work is small (>= ~128
+// pixel steps per wave)
+int vote_grid_steps(int64_t pixel_steps, const void *kernel) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0) per_cu = 4;
+    int64_t cap = (int64_t)cu_count() * per_cu;
+    int64_t need = (pixel_steps / 128 + 3) / 4;
     return (int)(need < 1 ? 1 : (need < cap ? need : cap));
 }
 
@@ -1073,12 +1360,13 @@ template <int KIND, bool EVD>
 struct CompactStage {
     static int run(const CompactArgs *a) {
         dim3 grid(a->nblk, a->b);
-        k_fg_count<KIND, EVD><<<grid, 256, 0, a->s>>>(a->m, a->H, a->W, a->ws.blkcnt, a->ws.fg, a->nblk);
-        k_fg_downsample<KIND, EVD><<<grid, 256, 0, a->s>>>(a->m, a->H, a->W, a->ws.fg, a->ws.dscnt, a->ws.tnds,
-                                                           a->nblk, a->min_num, a->max_num, a->seed, a->keep);
-        k_compact<KIND, EVD><<<grid, 256, 0, a->s>>>(a->m, a->vx, a->H, a->W, a->vn, a->ws.fg, a->ws.tnds,
-                                                     a->ws.blkcnt, a->ws.dscnt, a->nblk, a->min_num, a->max_num,
-                                                     a->seed, a->keep, a->ws.tn, a->ws.coords, a->ws.raw);
+        k_fg_count<KIND, EVD><<<grid, 256, 0, a->s>>>(a->m, a->H, a->W, a->ws.blkcnt, a->nblk, a->ws.counts,
+                                                      a->ws.zero_words);
+        k_fg_downsample<KIND, EVD><<<grid, 256, 0, a->s>>>(a->m, a->H, a->W, a->ws.blkcnt, a->ws.dscnt, a->nblk,
+                                                           a->min_num, a->max_num, a->seed, a->keep);
+        k_compact<KIND, EVD><<<grid, 256, 0, a->s>>>(a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.dscnt,
+                                                     a->nblk, a->min_num, a->max_num, a->seed, a->keep, a->ws.tn,
+                                                     a->ws.fgtot, a->ws.pex, a->ws.pix, a->ws.exotic, a->ws.nchv);
         return last();
     }
 };
@@ -1097,8 +1385,6 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
     const int b = img->b, H = img->H, W = img->W, vn = img->vn;
     const int64_t P = (int64_t)H * W;
     const int nblk = (int)((P + kCompactChunk - 1) / kCompactChunk);
-    hipError_t e = hipMemsetAsync(w.fg, 0, w.zero_bytes, s);
-    if (e != hipSuccess) return rc(e);
     CompactArgs ca;
     ca.m = MaskView{img->mask, img->mask_strides[0], img->mask_strides[1], img->mask_strides[2],
                     img->mask_strides[3]};
@@ -1113,30 +1399,23 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
     ca.s = s;
     int r = dispatch_mask<CompactStage>(img->mask_kind, evd, (const CompactArgs *)&ca);
     if (r) return r;
-    const int hgn = (nh + kVoteHG - 1) / kVoteHG;
-    int64_t ng = (int64_t)b * nh * vn;
-    k_generate<<<(unsigned)((ng + 255) / 256), 256, 0, s>>>(w.coords, w.raw, w.tn, P, b, vn, nh, prm->idxs,
-                                                          mix64(prm->seed), w.hyp, w.hypf, w.item_base, hgn,
-                                                          dg.hyp);
-    if ((r = last())) return r;
     VoteArgs va{};
-    va.coords = w.coords; va.coords_b = P;
-    va.raw = w.raw; va.raw_b = (int64_t)vn * P; va.raw_v = P; va.raw_t = 1;
-    va.hypf = w.hypf;
-    va.hyp = w.hyp; va.hyp_b = (int64_t)nh * vn;
-    va.counts = w.counts; va.cnt_b = (int64_t)vn * nh; va.cnt_v = nh; va.cnt_h = 1;
+    va.pix = w.pix; va.pex = w.pex; va.P = (int32_t)P;
+    va.exotic = w.exotic; va.exotic_b = (int32_t)w.nchv;
+    va.hyp = nullptr;
+    va.hyp_out = w.hyp; va.diag_hyp = dg.hyp;
+    va.idxs = prm->idxs; va.seed = mix64(prm->seed);
+    va.counts = w.counts; va.cnt_bs = vn * nh; va.cnt_v = nh; va.cnt_h = 1;
     va.tn_dev = w.tn; va.tn_host = 0;
-    va.item_base = w.item_base;
-    va.b = b; va.vn = vn; va.nh = nh; va.hgn = hgn;
-    va.thr = prm->inlier_thresh;
-    thresholds(prm->inlier_thresh, &va.thr_hi, &va.thr_lo);
-    // upper bound of the items: every pixel of every image in the foreground
-    int64_t items_ub = (int64_t)b * vn * hgn * ((P + kVoteChunk - 1) / kVoteChunk);
+    va.b = b; va.vn = vn; va.nh = nh; va.hgn = (nh + kGroup - 1) / kGroup;
+    fast_constants(prm->inlier_thresh, &va);
+    // upper bound of the work: every pixel of every image in the foreground
+    int64_t steps_ub = (int64_t)b * vn * va.hgn * P;
     if (dg.ev_vote_begin) {
         hipError_t e = hipEventRecord((hipEvent_t)dg.ev_vote_begin, s);
         if (e != hipSuccess) return rc(e);
     }
-    k_vote_count<<<vote_grid(items_ub), 256, 0, s>>>(va);
+    k_vote_count<true, true><<<vote_grid_steps(steps_ub, (const void *)k_vote_count<true, true>), 256, 0, s>>>(va);
     if ((r = last())) return r;
     if (dg.ev_vote_end) return rc(hipEventRecord((hipEvent_t)dg.ev_vote_end, s));
     return PV_OK;
@@ -1193,7 +1472,7 @@ int pv_voting_for_hypothesis(const float *direct, const float *coords, const flo
     if (tn == 0 || hn == 0) return PV_OK;
     float hi, lo;
     thresholds(inlier_thresh, &hi, &lo);
-    const int hgn = (hn + kVoteHG - 1) / kVoteHG;
+    const int hgn = (hn + kBytesHG - 1) / kBytesHG;
     int64_t items = (int64_t)vn * hgn * ((tn + kWave - 1) / kWave);
     hipStream_t s = (hipStream_t)stream;
     if (mode == PV_VOTE_DENSE)
@@ -1234,19 +1513,16 @@ int pv_vote_counts(const float *direct, const float *coords, const float *hypo, 
     hipError_t e = hipMemsetAsync(counts, 0, sizeof(int32_t) * (size_t)hn * vn, s);
     if (e != hipSuccess) return rc(e);
     VoteArgs va{};
-    va.coords = (const float2 *)coords; va.coords_b = 0;
-    va.raw = (const float2 *)direct; va.raw_b = 0; va.raw_v = 1; va.raw_t = vn;
-    va.hypf = nullptr;
-    va.hyp = (const float2 *)hypo; va.hyp_b = 0;
-    va.counts = counts; va.cnt_b = 0; va.cnt_v = 1; va.cnt_h = vn;
+    va.coords = (const float2 *)coords; va.P = tn;
+    va.raw = (const float2 *)direct; va.raw_v = 1; va.raw_t = vn;
+    va.hyp = (const float2 *)hypo;
+    va.counts = counts; va.cnt_bs = 0; va.cnt_v = 1; va.cnt_h = vn;
     va.tn_dev = nullptr; va.tn_host = tn;
-    va.item_base = nullptr;
-    va.b = 1; va.vn = vn; va.nh = hn; va.hgn = (hn + kVoteHG - 1) / kVoteHG;
-    va.thr = inlier_thresh;
-    thresholds(inlier_thresh, &va.thr_hi, &va.thr_lo);
+    va.b = 1; va.vn = vn; va.nh = hn; va.hgn = (hn + kGroup - 1) / kGroup;
+    fast_constants(inlier_thresh, &va);
     if (tn == 0) return PV_OK;
-    int64_t items = (int64_t)vn * va.hgn * ((tn + kVoteChunk - 1) / kVoteChunk);
-    k_vote_count<<<vote_grid(items), 256, 0, s>>>(va);
+    k_vote_count<false, false><<<vote_grid_steps((int64_t)vn * va.hgn * tn, (const void *)k_vote_count<false, false>),
+                                 256, 0, s>>>(va);
     return last();
 }
 
@@ -1269,10 +1545,9 @@ int pv_ransac_voting_v3(const pv_image_desc *img, const pv_vote_params *prm, flo
     if ((r = front_half(img, prm, nh, false, w, dg, s))) return r;
     const int b = img->b, vn = img->vn;
     const int64_t P = (int64_t)img->H * img->W;
-    k_refine<<<dim3(kRefineNJ, vn, b), 256, 0, s>>>(w.counts, w.hyp, w.coords, w.raw, w.tn, P, vn, nh,
-                                                    prm->inlier_thresh, w.win, w.ratio, w.best, w.refpart);
-    if ((r = last())) return r;
-    k_solve<<<b, 64, 0, s>>>(w.refpart, w.ratio, w.tn, vn, nh, prm->confidence, prm->max_iter, out, dg, w.win);
+    k_refine_solve<<<dim3(kRefineNJ, vn, b), 256, 0, s>>>(w.counts, w.hyp, w.pex, w.tn, P, vn, nh,
+                                                          prm->inlier_thresh, w.win, w.ratio, w.refpart, w.ticket,
+                                                          prm->confidence, prm->max_iter, out, dg);
     if ((r = last())) return r;
     if (dg.counts) {
         hipError_t e = hipMemcpyAsync(dg.counts, w.counts, sizeof(int32_t) * (size_t)b * vn * nh,
@@ -1304,7 +1579,7 @@ int pv_estimate_voting_distribution_with_mean(const pv_image_desc *img, const pv
     int nh = 0;
     int r = evd_front(img, prm, workspace, workspace_bytes, &w, &nh, s);
     if (r) return r;
-    k_evd_with_mean<<<dim3(img->vn, img->b), 256, 0, s>>>(w.counts, w.hyp, w.fg, w.tn, img->vn, nh, prm->min_num,
+    k_evd_with_mean<<<dim3(img->vn, img->b), 256, 0, s>>>(w.counts, w.hyp, w.fgtot, w.tn, img->vn, nh, prm->min_num,
                                                           prm->min_hyp_num, mean, cov);
     return last();
 }
@@ -1317,7 +1592,7 @@ int pv_estimate_voting_distribution(const pv_image_desc *img, const pv_vote_para
     int nh = 0;
     int r = evd_front(img, prm, workspace, workspace_bytes, &w, &nh, s);
     if (r) return r;
-    k_evd_topk<<<dim3(img->vn, img->b), 256, 0, s>>>(w.counts, w.hyp, w.fg, w.tn, img->vn, nh, prm->min_num,
+    k_evd_topk<<<dim3(img->vn, img->b), 256, 0, s>>>(w.counts, w.hyp, w.fgtot, w.tn, img->vn, nh, prm->min_num,
                                                      prm->topk, mean, cov);
     return last();
 }

