@@ -95,26 +95,16 @@ def main():
         raise SystemExit(f"keypoint error {err} px > 5 on the synthetic field (tn={tn})")
 
     seeds = [rank * 1_000_003 + 17 * k + 3 for k in range(K)]
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     s = torch.cuda.Stream(device=dev)
-    for a, b in ev:       # materialise the hipEvent_t handles before capture
-        a.record(s)
-        b.record(s)
-    torch.cuda.synchronize()
 
-    from pvnet_amd import _lib
-
-    def step(k, timed=True):
-        if timed:   # same call, plus hipEvents around the fused vote+count kernel
-            dd = _lib.V3Diag(ev_vote_begin=ev[k][0].cuda_event, ev_vote_end=ev[k][1].cuda_event)
-            return _raw_v3(rvg, seg, ver, args.hn, seeds[k], work, out[k], dd)
+    def step(k):
         return rvg.ransac_voting_layer_v3_from_network(seg, ver, args.hn, _seed=seeds[k], _workspace=work,
                                                        out=out[k])
 
-    # warmup (eager, also JIT-free: kernels are precompiled)
+    # warmup (eager; kernels are precompiled, nothing is JIT-compiled)
     with torch.cuda.stream(s):
         for i in range(args.warmup):
-            step(i % K, timed=False)
+            step(i % K)
     torch.cuda.synchronize()
 
     graph = None
@@ -149,7 +139,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    vote_ms = np.array([a.elapsed_time(b) for a, b in ev])
+    # dominant kernel's duration: hipEvents recorded by the library right
+    # before and after the vote kernel on the stream it is launched on, over
+    # eager replays of the same K steps (events inside a captured graph do not
+    # time the nodes between them)
+    vote_ms = time_vote_kernel(rvg, seg, ver, args.hn, seeds, work, out, s)
     res = dict(elapsed=elapsed, vote_ms=vote_ms, tn=tn)
     # sanity on the timed outputs
     final_err = float(np.abs(out.cpu().numpy() - fb["keypoints"][None]).max())
@@ -158,6 +152,20 @@ def main():
     if ws > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def time_vote_kernel(rvg, seg, ver, hn, seeds, work, out, stream):
+    from pvnet_amd import _lib
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in seeds]
+    with torch.cuda.stream(stream):
+        for a, b in ev:         # materialise the hipEvent_t handles
+            a.record(stream)
+            b.record(stream)
+        for k, (a, b) in enumerate(ev):
+            dd = _lib.V3Diag(ev_vote_begin=a.cuda_event, ev_vote_end=b.cuda_event)
+            _raw_v3(rvg, seg, ver, hn, seeds[k], work, out[k], dd)
+    torch.cuda.synchronize()
+    return np.array([a.elapsed_time(b) for a, b in ev])
 
 
 def _raw_v3(rvg, seg, ver, hn, seed, work, out, dd):

@@ -13,21 +13,24 @@
 // as explicit fmaf() calls.
 //
 // Design notes (DESIGN.md has the long form):
-//   * One wave = 64 lanes x 4 pixels of one keypoint v; the wave loops over a
-//     group of hypotheses that are wave-uniform (scalar loads).  The inlier
-//     decision of each (h, pixel) is a v_cmp whose 64-bit result is the
-//     ballot, so the per-hypothesis inlier count is s_bcnt1 + s_add on the
-//     scalar unit: no [hn,vn,tn] mask is ever materialised on the v3 path.
-//   * The vote test runs a division- and sqrt-free approximation (rsq) with a
-//     rigorous error bound; pairs inside the guard band around the threshold
-//     (and hypotheses/pixels outside the bound's domain) are re-decided with
-//     the reference's exact IEEE sequence, so every decision is bit-identical
-//     to KU:116-125.
+//   * The (hypothesis, pixel) vote test runs in the pixel's rotated frame:
+//     5 FMAs and a compare, no sqrt or division.  A rigorous error bound
+//     puts a guard band around the threshold; pairs inside it, and
+//     hypotheses / pixels outside the bound's domain, are re-decided with
+//     the reference's exact IEEE sequence (KU:116-125), so every decision is
+//     bit-identical to the reference's.
+//   * v3 / EVD never materialise the [hn,vn,tn] inlier mask: the fused
+//     vote/count kernel keeps per-hypothesis counts in registers (lane =
+//     hypothesis, pixels broadcast from LDS).  The byte mask is produced only
+//     by the API entry point voting_for_hypothesis, as coalesced 8-byte
+//     stores (lane = 8 pixels, hypotheses broadcast from LDS).
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../../include/pvvote.h"
@@ -38,12 +41,8 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kCompactChunk = 1024;          // pixels per compaction block (256 threads x 4)
-constexpr int kVotePix = 4;                  // pixels per lane in the vote waves
-constexpr int kVoteChunk = kWave * kVotePix; // 256 pixels per vote item
+constexpr int kVoteChunk = 256;              // pixels per LDS-staged sub-chunk of the vote waves
 constexpr int kRefineNJ = 16;                // refine blocks per (image, keypoint)
-constexpr int kBytesHG = 128;                // hypotheses per item of the byte-output vote kernel
-// |fast - reference| <= 15 ulp(1) ~ 9e-7; the band is 4.4x wider.
-constexpr float kGuard = 4.0e-6f;
 // domain of the fast test's error bound
 constexpr float kHypMax = 1.0e17f;           // |hx|,|hy| above -> exact-only hypothesis
 constexpr float kLattice = 2.5e-6f;          // |h - round(h)| below (both axes) -> exact-only
@@ -90,37 +89,6 @@ __device__ __forceinline__ bool hyp_exact_only(float hx, float hy) {
     bool big = !(fabsf(hx) <= kHypMax) || !(fabsf(hy) <= kHypMax);   // also NaN/inf
     bool lat = fabsf(hx - rintf(hx)) < kLattice && fabsf(hy - rintf(hy)) < kLattice;
     return big || lat;
-}
-
-// --------------------------------------------------------------------------
-// per-pixel data of the fast test
-// --------------------------------------------------------------------------
-struct Pix {
-    float cx, cy;   // exact pixel centre (coords)
-    float nx, ny;   // raw predicted direction
-    float fx;       // cx, or NaN when the pixel must take the exact path
-    float ux, uy;   // approximately normalised direction
-};
-
-__device__ __forceinline__ Pix make_pix(float cx, float cy, float nx, float ny) {
-    Pix p;
-    p.cx = cx; p.cy = cy; p.nx = nx; p.ny = ny;
-    float n1 = sqrtf(nx * nx + ny * ny);                 // exactly the reference's norm1
-    bool ok = !((double)n1 < 1e-6) && (n1 <= kN1Max);    // NaN -> not ok
-    float s = sqrtf(fmaf(nx, nx, ny * ny));
-    p.ux = nx / s;
-    p.uy = ny / s;
-    p.fx = ok ? cx : __builtin_nanf("");
-    return p;
-}
-
-// Approximate cosine of the fast test: rel. error <= ~7 ulp(1) on its domain.
-__device__ __forceinline__ float fast_cos(const Pix &p, float hx, float hy) {
-    float dx = hx - p.fx;
-    float dy = hy - p.cy;
-    float dd = fmaf(dy, dy, dx * dx);
-    float num = fmaf(dy, p.uy, dx * p.ux);
-    return num * __builtin_amdgcn_rsqf(dd);
 }
 
 __device__ __forceinline__ uint64_t ballot(bool x) { return __ballot(x); }
@@ -468,6 +436,7 @@ struct VoteArgs {
     int32_t P, raw_v, raw_t, exotic_b, cnt_v, cnt_h, cnt_bs;
     int32_t tn_host, b, vn, nh, hgn, fast;
     float thr, tau, gzf, gzr;
+    uint64_t *trace;            // debug: per-wave (start, end) s_memrealtime stamps, or nullptr
 };
 
 // the reference's operands of pixel t: (cx, cy, nx, ny)
@@ -554,8 +523,32 @@ __device__ __forceinline__ bool pixel_exotic(float nx, float ny) {
 constexpr int kHypLane = 2;
 constexpr int kGroup = kWave * kHypLane;
 
+// The wave's slab of exact operands.  Pipeline pixels are integer centres
+// below 65536 (check_desc), packed as cx | cy << 16: 12 B per pixel keeps a
+// block at 28 KiB of LDS (5 blocks per CU); API coordinates are any floats.
+template <bool PACKED>
+struct ExactSlab {
+    float2 n[kVoteChunk];
+    uint32_t c[kVoteChunk];
+    __device__ __forceinline__ void put(int j, const F4 &e) {
+        n[j] = make_float2(e.z, e.w);
+        c[j] = (uint32_t)e.x | ((uint32_t)e.y << 16);
+    }
+    __device__ __forceinline__ F4 get(int j) const {
+        const float2 d = n[j];
+        const uint32_t q = c[j];
+        return F4{(float)(q & 0xffffu), (float)(q >> 16), d.x, d.y};
+    }
+};
+template <>
+struct ExactSlab<false> {
+    F4 e[kVoteChunk];
+    __device__ __forceinline__ void put(int j, const F4 &x) { e[j] = x; }
+    __device__ __forceinline__ F4 get(int j) const { return e[j]; }
+};
+
 template <bool GEN, bool PREPPED>
-__device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, F4 *stagex, int b, int v, int hg, int ts,
+__device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, ExactSlab<PREPPED> &stagex, int b, int v, int hg, int ts,
                                              int te, int n) {
     const int lane = lane_id();
     const float tau = a.tau;
@@ -597,7 +590,7 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, F4 *s
                     q = F4{f.x, f.y, f.z, f.w};
                     exo_p |= pixel_exotic(e.z, e.w);
                 }
-                stagex[j] = e;
+                stagex.put(j, e);
                 xl[k] = e.x;
                 xh[k] = e.x;
             }
@@ -687,7 +680,7 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, F4 *s
                     const float hxi = i1 ? hx[1] : hx[0], hyi = i1 ? hy[1] : hy[0], gdi = i1 ? gd[1] : gd[0];
                     const bool u = fabsf(zval(stage[j + p], hxi, hyi)) <= gdi;
                     if (__builtin_amdgcn_ballot_w64(u)) {
-                        const F4 e = stagex[j + p];
+                        const F4 e = stagex.get(j + p);
                         const float ex = i1 ? he[1].x : he[0].x, ey = i1 ? he[1].y : he[0].y;
                         const int r = (u && exact_vote(e.z, e.w, e.x, e.y, ex, ey, a.thr)) ? 1 : 0;
                         cnt[0] += i1 ? 0 : r;
@@ -740,7 +733,7 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, F4 *s
                         const int jj = k * kWave + lane;
                         bool e = false;
                         if (jj < np) {
-                            const F4 x = stagex[jj];
+                            const F4 x = stagex.get(jj);
                             e = exact_vote(x.z, x.w, x.x, x.y, ex, ey, a.thr);
                         }
                         c += __popcll(__builtin_amdgcn_ballot_w64(e));
@@ -752,7 +745,7 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, F4 *s
             // every pair through the reference sequence
 #pragma unroll 1
             for (int j = 0; j < np; ++j) {
-                const F4 e = stagex[j];
+                const F4 e = stagex.get(j);
 #pragma unroll
                 for (int i = 0; i < kHypLane; ++i) cnt[i] += exact_vote(e.z, e.w, e.x, e.y, he[i].x, he[i].y, a.thr);
             }
@@ -772,13 +765,14 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, F4 *s
 // ranges, one per wave, so every wave does the same number of pixel steps and
 // generates each group's hypotheses once per range.
 template <bool GEN, bool PREPPED>
-__global__ __launch_bounds__(256) void k_vote_count(VoteArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) void k_vote_count(VoteArgs a) {
     const int wave = uniform((int)(blockIdx.x * 4 + threadIdx.x / 64));
     const int64_t nwaves = (int64_t)gridDim.x * 4;
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     __shared__ F4 stage_all[4][kVoteChunk];
-    __shared__ F4 stagex_all[4][kVoteChunk];
+    __shared__ ExactSlab<PREPPED> stagex_all[4];
     F4 *stage = stage_all[threadIdx.x / 64];
-    F4 *stagex = stagex_all[threadIdx.x / 64];
+    ExactSlab<PREPPED> &stagex = stagex_all[threadIdx.x / 64];
     int64_t total = 0;
     for (int b = 0; b < a.b; ++b) total += (int64_t)a.vn * a.hgn * (a.tn_dev ? a.tn_dev[b] : a.tn_host);
     int64_t lo = total * wave / nwaves, hi = total * (wave + 1) / nwaves;
@@ -797,6 +791,13 @@ __global__ __launch_bounds__(256) void k_vote_count(VoteArgs a) {
         vote_segment<GEN, PREPPED>(a, stage, stagex, uniform(b), uniform(v), uniform(hg), uniform(ts), uniform(te),
                                    n);
         lo += te - ts;
+    }
+    if (a.trace && lane_id() == 0) {
+        uint32_t hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        a.trace[wave * 3] = t_start;
+        a.trace[wave * 3 + 1] = __builtin_amdgcn_s_memrealtime();
+        a.trace[wave * 3 + 2] = hw;
     }
 }
 
@@ -1162,46 +1163,287 @@ __global__ __launch_bounds__(256) void k_generate_api(const float *direct, const
     hypo[hi * vn * 2 + vi * 2 + 1] = y;
 }
 
-// KU:88-167 with byte outputs.  One lane per pixel of one keypoint, hypotheses
-// wave-uniform; mode OR writes only the inlier bytes (reference semantics),
-// DENSE writes every byte.
+// KU:88-167 with byte outputs: inliers[h][v][t] (U1, store-bound: hn*vn*tn
+// bytes).  Mode OR writes only the inlier bytes (reference semantics: the
+// caller's buffer keeps its other bytes), DENSE writes every byte.
+//
+// Rows (h, v) start at arbitrary byte offsets R = (h*vn + v)*tn, but rows of
+// hypotheses h = c (mod 8) share s = R mod 8.  A wave takes rows of one
+// keypoint v and one class c inside one 512-byte window w: lane l owns the
+// 8-byte aligned word at R - s + 512w + 8l -- pixels t = 512w - s + 8l + j,
+// j < 8 -- and writes it with one 8-byte store per row.  The work is the
+// linearised (v, c, w, row) space cut into equal ranges, one per wave, rows
+// fastest, so a wave prepares its pixels once per (c, w) segment.  A prepass
+// (k_prep_api) lays the operands out for contiguous reads: pixels keypoint-
+// major as (ux, uy, cx, cy), hypotheses keypoint- and class-major.  The vote
+// test is vote_segment's rotated-frame test (5 FMAs per pair); the inlier
+// bytes are the sign bytes of z gathered with v_perm.  Pairs inside the
+// guard band, and hypotheses / pixels outside the fast domain, take the
+// reference's exact sequence.
+constexpr int kBytePix = 8;
+constexpr int kByteWin = kWave * kBytePix;      // bytes of a row per segment
+constexpr int kByteHB = 64;                      // hypothesis records per batch
+
+struct ByteArgs {
+    const float4 *prep;    // [vn][tn] (ux, uy, cx, cy), see k_prep_api
+    const float2 *hypc;    // [vn][hn] class-major: hypothesis c + 8i at [v][cbase(c) + i]
+    const float *direct;   // [tn][vn][2]
+    const float *coords;   // [tn][2]
+    const float *hypo;     // [hn][vn][2]
+    uint8_t *out;          // [hn][vn][tn]
+    int tn, vn, hn, nwin, fast;
+    float thr, tau, gzf, gzr;
+};
+
+__host__ __device__ inline int class_rows(int hn, int c) { return c < hn ? (hn - c + 7) / 8 : 0; }
+__host__ __device__ inline int class_base(int hn, int c) {   // rows of classes < c
+    int b = 0;
+    for (int k = 0; k < c; ++k) b += class_rows(hn, k);
+    return b;
+}
+
+// Operand layouts of the byte-output kernel.  Pixel (t, v): (ux, uy, cx, cy)
+// with u the direction rounded per component; (0, 0) for a pixel that never
+// votes (norm1 < 1e-6 or NaN, KU:119-121, or non-finite coordinates) and
+// ux = NaN for one outside the fast domain.  Hypotheses regrouped by class.
+__global__ __launch_bounds__(256) void k_prep_api(const float *direct, const float *coords, const float *hypo,
+                                                  float4 *prep, float2 *hypc, int tn, int vn, int hn) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t np = (int64_t)vn * tn;
+    if (i < np) {
+        const int v = (int)(i / tn), t = (int)(i - (int64_t)v * tn);
+        const float2 c = *(const float2 *)(coords + (int64_t)t * 2);
+        const float2 d = *(const float2 *)(direct + ((int64_t)t * vn + v) * 2);
+        const float n1 = sqrtf(d.x * d.x + d.y * d.y);
+        const bool ok = !((double)n1 < 1e-6) && n1 == n1 && isfinite(c.x) && isfinite(c.y);
+        const float rs = __builtin_amdgcn_rsqf(fmaf(d.x, d.x, d.y * d.y));
+        float4 q = make_float4(0.f, 0.f, c.x, c.y);
+        if (ok)
+            q = (n1 <= kN1Max) ? make_float4(d.x * rs, d.y * rs, c.x, c.y)
+                               : make_float4(__builtin_nanf(""), 0.f, c.x, c.y);
+        prep[i] = q;
+    } else if (i < np + (int64_t)vn * hn) {
+        const int64_t k = i - np;
+        const int v = (int)(k / hn), h = (int)(k - (int64_t)v * hn);
+        const int c = h & 7;
+        hypc[(int64_t)v * hn + class_base(hn, c) + (h >> 3)] = *(const float2 *)(hypo + ((int64_t)h * vn + v) * 2);
+    }
+}
+
+// rows [i0, i1) (i1 - i0 <= kByteHB) of keypoint v, class c, window w
 template <int MODE>
-__global__ __launch_bounds__(256) void k_vote_bytes(const float *direct, const float *coords, const float *hypo,
-                                                    uint8_t *inliers, int tn, int vn, int hn, float thr, float thr_hi,
-                                                    float thr_lo, int hgn) {
-    const int wave = uniform((int)(blockIdx.x * 4 + threadIdx.x / 64));
+__device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, int v, int c, int w, int i0, int i1) {
     const int lane = lane_id();
-    const int nch = (tn + kWave - 1) / kWave;
-    const int total = vn * hgn * nch;
-    for (int item = wave; item < total; item += gridDim.x * 4) {
-        int hg = item % hgn;
-        int r = item / hgn;
-        int chunk = r % nch;
-        int v = r / nch;
-        int t = chunk * kWave + lane;
-        bool in = t < tn;
-        int tt = in ? t : 0;
-        float nx = direct[(int64_t)tt * vn * 2 + v * 2], ny = direct[(int64_t)tt * vn * 2 + v * 2 + 1];
-        if (!in) { nx = 0.f; ny = 0.f; }
-        Pix px = make_pix(coords[tt * 2], coords[tt * 2 + 1], nx, ny);
-        int h0 = hg * kBytesHG, h1 = min(h0 + kBytesHG, hn);
-        for (int h = h0; h < h1; ++h) {
-            float ex_x = hypo[(h * vn + v) * 2], ex_y = hypo[(h * vn + v) * 2 + 1];
-            bool exo = hyp_exact_only(ex_x, ex_y);
-            float hx = exo ? __builtin_nanf("") : ex_x, hy = exo ? __builtin_nanf("") : ex_y;
-            float cs = fast_cos(px, hx, hy);
-            bool hi = cs > thr_hi;
-            bool may = !(cs <= thr_lo);
-            bool res = hi;
-            if (ballot(may && !hi && in)) {
-                if (may && !hi) res = exact_vote(px.nx, px.ny, px.cx, px.cy, ex_x, ex_y, thr);
-            }
-            if (in) {
-                uint8_t *o = inliers + ((int64_t)h * vn + v) * tn + t;
-                if (MODE == PV_VOTE_DENSE) *o = res ? 1 : 0;
-                else if (res) *o = 1;
+    const float tau = a.tau;
+    const int nh = i1 - i0;
+    const int h0 = c + 8 * i0;                                  // rows h0 + 8i, i < nh
+    const int64_t R0 = ((int64_t)h0 * a.vn + v) * a.tn;
+    const int s = (int)(R0 & 7);
+    const int tb = kByteWin * w - s + kBytePix * lane;          // lane's first pixel
+    const int64_t rstep = (int64_t)8 * a.vn * a.tn;             // R(h + 8) - R(h)
+    uint8_t *orow = a.out + R0 - s + (int64_t)kByteWin * w + kBytePix * lane;   // 8-byte aligned
+
+    // ---- operands: all loads issued together ----
+    float2 hq = make_float2(0.f, 0.f);
+    if (lane < nh) hq = a.hypc[(int64_t)v * a.hn + class_base(a.hn, c) + i0 + lane];
+    uint32_t vmask = 0, okmask = 0;
+    bool exo = false;
+    float fu[kBytePix], fv[kBytePix], fk1[kBytePix], fk2[kBytePix];   // (ux, uy, cx, cy) first
+    const float4 *pp = a.prep + (int64_t)v * a.tn;
+#pragma unroll
+    for (int j = 0; j < kBytePix; ++j) {
+        const int t = tb + j;
+        fu[j] = fv[j] = fk1[j] = fk2[j] = 0.f;
+        if (t >= 0 && t < a.tn) {
+            const float4 q = pp[t];
+            fu[j] = q.x; fv[j] = q.y; fk1[j] = q.z; fk2[j] = q.w;
+            vmask |= 1u << j;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kBytePix; ++j) {
+        exo |= fu[j] != fu[j];                                  // outside the fast domain
+        if (fu[j] != 0.f || fv[j] != 0.f) okmask |= 1u << j;    // votes at all
+    }
+    const bool slow = __builtin_amdgcn_readfirstlane(!a.fast || __builtin_amdgcn_ballot_w64(exo) != 0);
+    // origin: an integer point at the first voting pixel; R >= |c - o| over the voting pixels
+    const uint64_t anyok = __builtin_amdgcn_ballot_w64(okmask != 0);
+    float ox = 0.f, oy = 0.f, Rw = 0.f;
+    if (anyok) {
+        const int l0 = __builtin_ctzll(anyok);
+        const int j0 = __builtin_ctz(__builtin_amdgcn_readlane(okmask, l0));
+        float fx = fk1[0], fy = fk2[0];
+#pragma unroll
+        for (int j = 1; j < kBytePix; ++j)
+            if (j == j0) { fx = fk1[j]; fy = fk2[j]; }
+        ox = floorf(bcast(fx, l0));
+        oy = floorf(bcast(fy, l0));
+        float r2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < kBytePix; ++j)
+            if (okmask >> j & 1) r2 = fmaxf(r2, fmaf(fk1[j] - ox, fk1[j] - ox, (fk2[j] - oy) * (fk2[j] - oy)));
+        Rw = __builtin_amdgcn_sqrtf(wave_max(r2)) * 1.00001f;
+    }
+    // fast operands (ux, uy, -k1, -k2) relative to the origin, in place;
+    // pixels that never vote get u = 0, -k1 = -1e30: z = -1e30 tau, far
+    // below the band, for every finite h'
+#pragma unroll
+    for (int j = 0; j < kBytePix; ++j) {
+        const bool ok = okmask >> j & 1;
+        const float ux = fu[j], uy = fv[j];
+        const float cx = fk1[j] - ox, cy = fk2[j] - oy;
+        fu[j] = ok ? ux : 0.f;
+        fv[j] = ok ? uy : 0.f;
+        fk1[j] = ok ? -fmaf(ux, cx, uy * cy) : -1.0e30f;
+        fk2[j] = ok ? -fmaf(ux, cy, -(uy * cx)) : 0.f;
+    }
+    // hypothesis records (lane i -> row h0 + 8i): h - o, band, exact flag
+    {
+        F4 rec{0.f, 0.f, 0.f, 1.f};
+        if (lane < nh) {
+            // non-finite or outside the fast domain: the exact sequence decides
+            const bool xo = !(isfinite(hq.x) && isfinite(hq.y)) || hyp_exact_only(hq.x, hq.y);
+            if (!xo && !slow) {
+                const float hx = hq.x - ox, hy = hq.y - oy;
+                const float B = (__builtin_amdgcn_sqrtf(fmaf(hx, hx, hy * hy)) + Rw) * 1.00001f + 1e-30f;
+                rec = F4{hx, hy, (a.gzf + a.gzr) * B * 1.00001f, 0.f};
             }
         }
+        __builtin_amdgcn_wave_barrier();
+        recs[lane] = rec;
+        __builtin_amdgcn_wave_barrier();
+    }
+
+    // the reference's decision of pixel j against row h (rare paths)
+    auto exact_at = [&](int j, int h) {
+        int t = tb + j;
+        asm volatile("" : "+v"(t));   // keep the address math here: not hoisted into live registers
+        const float2 q = *(const float2 *)(a.hypo + ((int64_t)h * a.vn + v) * 2);
+        const float2 cc = *(const float2 *)(a.coords + (int64_t)t * 2);
+        const float2 d = *(const float2 *)(a.direct + ((int64_t)t * a.vn + v) * 2);
+        return exact_vote(d.x, d.y, cc.x, cc.y, q.x, q.y, a.thr);
+    };
+    auto store = [&](uint8_t *p, uint32_t lo, uint32_t hi) {
+        if (vmask == 0xffu) {
+            if (MODE == PV_VOTE_DENSE) {
+                *(uint2 *)p = make_uint2(lo, hi);
+            } else {
+                // KU:125 sets inlier bytes to 1 and leaves the others
+                const uint2 old = *(const uint2 *)p;
+                *(uint2 *)p = make_uint2((old.x & ~(lo * 0xffu)) | lo, (old.y & ~(hi * 0xffu)) | hi);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < kBytePix; ++j) {
+                if (vmask >> j & 1) {
+                    const uint8_t bit = (uint8_t)(((j < 4 ? lo : hi) >> (8 * (j & 3))) & 1u);
+                    if (MODE == PV_VOTE_DENSE) p[j] = bit;
+                    else if (bit) p[j] = 1;
+                }
+            }
+        }
+    };
+    // byte k of perm(hi, lo, sel) = byte sel_k of {hi, lo}: the sign bytes of four z's
+    constexpr uint32_t kSel01 = 0x0c0c0703u;   // z0.b3 -> b0, z1.b3 -> b1 (perm(z1, z0))
+    constexpr uint32_t kSel23 = 0x05040100u;   // p01.b0,b1 -> b0,b1; p23.b0,b1 -> b2,b3
+    auto pack4 = [&](float z0, float z1, float z2, float z3) {
+        const uint32_t p01 = __builtin_amdgcn_perm(__float_as_uint(z1), __float_as_uint(z0), kSel01);
+        const uint32_t p23 = __builtin_amdgcn_perm(__float_as_uint(z3), __float_as_uint(z2), kSel01);
+        const uint32_t sg = __builtin_amdgcn_perm(p23, p01, kSel23);
+        return (~sg & 0x80808080u) >> 7;            // 1 where z > 0 (band pairs are fixed below)
+    };
+
+    auto zrow = [&](const F4 &rec, float z[kBytePix]) {
+        float m = 3.0e38f;
+#pragma unroll
+        for (int j = 0; j < kBytePix; ++j) {
+            const float xr = fmaf(fu[j], rec.x, fmaf(fv[j], rec.y, fk1[j]));
+            const float yr = fmaf(fu[j], rec.y, fmaf(-fv[j], rec.x, fk2[j]));
+            z[j] = fmaf(xr, tau, -fabsf(yr));
+            m = fminf(m, fabsf(z[j]));
+        }
+        return m;
+    };
+
+    // Hot loop: the fast decision of every pair, one 8-byte store per row
+    // (byte stores for the partial words at row ends).  Rows with a pair
+    // inside the band and rows outside the fast domain are deferred to the
+    // exact pass below, which writes them instead -- the hot loop carries no
+    // exact-sequence code.
+    uint64_t dmask = 0;                                 // deferred rows (nh <= 64)
+    F4 rec = recs[0];
+    for (int i = 0; i < nh; ++i) {
+        const F4 nrec = recs[min(i + 1, kByteHB - 1)];    // next record, one iteration ahead
+        float z[kBytePix];
+        const float m = zrow(rec, z);
+        const bool d = __builtin_amdgcn_readfirstlane(__float_as_uint(rec.w)) ||
+                       __builtin_amdgcn_ballot_w64(m <= rec.z) != 0;
+        if (d) dmask |= 1ull << i;
+        else store(orow + rstep * i, pack4(z[0], z[1], z[2], z[3]), pack4(z[4], z[5], z[6], z[7]));
+        rec = nrec;
+    }
+
+    // Exact pass over the deferred rows.
+    while (dmask) {
+        const int i = __builtin_ctzll(dmask);
+        dmask &= dmask - 1;
+        const F4 r = recs[i];
+        uint32_t lo = 0, hi = 0;
+        if (__builtin_amdgcn_readfirstlane(__float_as_uint(r.w))) {
+            // row outside the fast domain: every pair exact
+#pragma unroll 1
+            for (int j = 0; j < kBytePix; ++j) {
+                const uint32_t bit = ((vmask >> j & 1) && exact_at(j, h0 + 8 * i)) ? 1u : 0u;
+                if (j < 4) lo |= bit << (8 * j);
+                else hi |= bit << (8 * (j - 4));
+            }
+        } else {
+            float z[kBytePix];
+            zrow(r, z);
+            lo = pack4(z[0], z[1], z[2], z[3]);
+            hi = pack4(z[4], z[5], z[6], z[7]);
+#pragma unroll 1
+            for (int j = 0; j < kBytePix; ++j) {
+                float zj = z[0];
+#pragma unroll
+                for (int k = 1; k < kBytePix; ++k) zj = j == k ? z[k] : zj;
+                const bool u = (vmask >> j & 1) && fabsf(zj) <= r.z;
+                if (__builtin_amdgcn_ballot_w64(u)) {
+                    if (u) {
+                        const uint32_t bit = 1u << (8 * (j & 3));
+                        const bool e = exact_at(j, h0 + 8 * i);
+                        if (j < 4) lo = e ? (lo | bit) : (lo & ~bit);
+                        else hi = e ? (hi | bit) : (hi & ~bit);
+                    }
+                }
+            }
+        }
+        store(orow + rstep * i, lo, hi);
+    }
+}
+
+// Balanced persistent waves over the linearised (v, c, window, row) space.
+template <int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_vote_bytes(ByteArgs a) {
+    __shared__ F4 recs_all[4][kByteHB];
+    F4 *recs = recs_all[threadIdx.x / 64];
+    const int wave = uniform((int)(blockIdx.x * 4 + threadIdx.x / 64));
+    const int64_t nwaves = (int64_t)gridDim.x * 4;
+    const int64_t per_v = (int64_t)a.nwin * a.hn;          // sum over c of nwin * class_rows(c)
+    const int64_t total = per_v * a.vn;
+    int64_t lo = total * wave / nwaves, hi = total * (wave + 1) / nwaves;
+    while (lo < hi) {
+        const int v = (int)(lo / per_v);
+        int64_t r = lo - (int64_t)v * per_v;
+        int c = 0;
+        while (r >= (int64_t)a.nwin * class_rows(a.hn, c)) { r -= (int64_t)a.nwin * class_rows(a.hn, c); ++c; }
+        const int nc = class_rows(a.hn, c);
+        const int w = (int)(r / nc);
+        const int i0 = (int)(r - (int64_t)w * nc);
+        const int i1 = (int)min<int64_t>((int64_t)nc, min<int64_t>(i0 + kByteHB, i0 + (hi - lo)));
+        if (kByteWin * w - (int)((((int64_t)c * a.vn + v) * a.tn) & 7) < a.tn)   // window inside the row
+            vote_bytes_seg<MODE>(a, recs, uniform(v), uniform(c), uniform(w), uniform(i0), uniform(i1));
+        lo += i1 - i0;
     }
 }
 
@@ -1273,11 +1515,6 @@ int cu_count() {
 inline int rc(hipError_t e) { return e == hipSuccess ? PV_OK : (int)e; }
 inline int last() { return rc(hipGetLastError()); }
 
-void thresholds(float thr, float *hi, float *lo) {
-    *hi = thr + kGuard;
-    *lo = thr - kGuard;
-}
-
 // Constants of the rotated-frame test (DESIGN.md "Exactness of the fast vote
 // test"): tau = sqrt(1-thr^2)/thr; band = gzf * B + gzr * D with
 // B >= |h - o| + |c - o| and D >= |h - c|:
@@ -1306,13 +1543,6 @@ void fast_constants(float thr, VoteArgs *va) {
     }
 }
 
-int vote_grid(int64_t items) {
-    // at most 8 waves per SIMD resident: 256 CUs x 32 waves = 8192 waves = 2048 blocks
-    int64_t cap = (int64_t)cu_count() * 8;
-    int64_t need = (items + 3) / 4;
-    return (int)(need < 1 ? 1 : (need < cap ? need : cap));
-}
-
 // persistent vote grid: every block resident at once (the occupancy limit of
 // the kernel: LDS slabs, registers), fewer when the work is small (>= ~128
 // pixel steps per wave)
@@ -1323,6 +1553,8 @@ int vote_grid_steps(int64_t pixel_steps, const void *kernel) {
     int64_t need = (pixel_steps / 128 + 3) / 4;
     return (int)(need < 1 ? 1 : (need < cap ? need : cap));
 }
+
+uint64_t *g_vote_trace = nullptr;   // debug hook (pv_debug_set_vote_trace)
 
 struct Launch {
     int kind;
@@ -1374,6 +1606,7 @@ struct CompactStage {
 int check_desc(const pv_image_desc *img) {
     if (!img || !img->mask || !img->vertex) return PV_EINVAL;
     if (img->b <= 0 || img->H <= 0 || img->W <= 0 || img->vn <= 0 || img->vn > 64) return PV_EINVAL;
+    if (img->H > 65535 || img->W > 65535) return PV_EINVAL;   // pixel centres pack into 16 bits
     if (img->mask_kind < PV_MASK_I64 || img->mask_kind > PV_MASK_SEG_F16) return PV_EINVAL;
     if (img->vertex_kind != PV_VERTEX_F32 && img->vertex_kind != PV_VERTEX_F16) return PV_EINVAL;
     return PV_OK;
@@ -1409,6 +1642,7 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
     va.tn_dev = w.tn; va.tn_host = 0;
     va.b = b; va.vn = vn; va.nh = nh; va.hgn = (nh + kGroup - 1) / kGroup;
     fast_constants(prm->inlier_thresh, &va);
+    va.trace = g_vote_trace;
     // upper bound of the work: every pixel of every image in the foreground
     int64_t steps_ub = (int64_t)b * vn * va.hgn * P;
     if (dg.ev_vote_begin) {
@@ -1470,18 +1704,29 @@ int pv_voting_for_hypothesis(const float *direct, const float *coords, const flo
     if (!direct || !coords || !hypo || !inliers || tn < 0 || vn <= 0 || hn < 0) return PV_EINVAL;
     if (mode != PV_VOTE_OR && mode != PV_VOTE_DENSE) return PV_EINVAL;
     if (tn == 0 || hn == 0) return PV_OK;
-    float hi, lo;
-    thresholds(inlier_thresh, &hi, &lo);
-    const int hgn = (hn + kBytesHG - 1) / kBytesHG;
-    int64_t items = (int64_t)vn * hgn * ((tn + kWave - 1) / kWave);
+    VoteArgs fc{};
+    fast_constants(inlier_thresh, &fc);
     hipStream_t s = (hipStream_t)stream;
+    // stream-ordered scratch for the prepass layouts: safe for concurrent streams and graph capture
+    const size_t prep_bytes = sizeof(float4) * (size_t)vn * tn, hyp_bytes = sizeof(float2) * (size_t)vn * hn;
+    char *scratch = nullptr;
+    hipError_t e = hipMallocAsync((void **)&scratch, prep_bytes + hyp_bytes, s);
+    if (e != hipSuccess) return rc(e);
+    ByteArgs ba{(const float4 *)scratch, (const float2 *)(scratch + prep_bytes), direct, coords, hypo, inliers,
+                tn, vn, hn, 0, fc.fast, fc.thr, fc.tau, fc.gzf, fc.gzr};
+    ba.nwin = (tn + 7 + kByteWin - 1) / kByteWin;
+    const int64_t nprep = (int64_t)vn * tn + (int64_t)vn * hn;
+    k_prep_api<<<(unsigned)((nprep + 255) / 256), 256, 0, s>>>(direct, coords, hypo, (float4 *)scratch,
+                                                                (float2 *)(scratch + prep_bytes), tn, vn, hn);
+    // persistent grid: every block resident, >= ~16 rows per wave
+    const int64_t rows = (int64_t)vn * ba.nwin * hn;
     if (mode == PV_VOTE_DENSE)
-        k_vote_bytes<PV_VOTE_DENSE><<<vote_grid(items), 256, 0, s>>>(direct, coords, hypo, inliers, tn, vn, hn,
-                                                                     inlier_thresh, hi, lo, hgn);
+        k_vote_bytes<PV_VOTE_DENSE><<<vote_grid_steps(rows * 8, (const void *)k_vote_bytes<PV_VOTE_DENSE>), 256, 0, s>>>(ba);
     else
-        k_vote_bytes<PV_VOTE_OR><<<vote_grid(items), 256, 0, s>>>(direct, coords, hypo, inliers, tn, vn, hn,
-                                                                  inlier_thresh, hi, lo, hgn);
-    return last();
+        k_vote_bytes<PV_VOTE_OR><<<vote_grid_steps(rows * 8, (const void *)k_vote_bytes<PV_VOTE_OR>), 256, 0, s>>>(ba);
+    int r = last();
+    e = hipFreeAsync(scratch, s);
+    return r ? r : rc(e);
 }
 
 int pv_generate_hypothesis_vp(const float *direct, const float *coords, const int32_t *idxs, float *hypo,
@@ -1525,6 +1770,9 @@ int pv_vote_counts(const float *direct, const float *coords, const float *hypo, 
                                  256, 0, s>>>(va);
     return last();
 }
+
+// debug only (not in pvvote.h): per-wave timestamps of the next pipeline vote launches
+void pv_debug_set_vote_trace(uint64_t *buf) { g_vote_trace = buf; }
 
 size_t pv_v3_workspace_size(int32_t b, int32_t H, int32_t W, int32_t vn, int32_t n_hyp) {
     if (b <= 0 || H <= 0 || W <= 0 || vn <= 0 || n_hyp <= 0) return 0;

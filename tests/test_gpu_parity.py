@@ -309,3 +309,25 @@ def test_graph_capture(device, rvg):
     gph.replay()
     torch.cuda.synchronize()
     np.testing.assert_array_equal(out.cpu().numpy(), ref.cpu().numpy())
+
+
+def test_fractional_coordinates_and_ragged_rows(device, rv):
+    """API inputs with non-integer coordinates (c - o is rounded in the fast
+    test) and row lengths that are not multiples of 8 (every byte-row start
+    alignment); bytes and counts equal the reference decisions."""
+    rng = np.random.default_rng(7)
+    for tn in (1, 7, 513, 1029):
+        vn, hn = 2, 37
+        coords = (np.stack([rng.uniform(0, 640, tn), rng.uniform(0, 480, tn)], 1)).astype(np.float32)
+        kp = np.array([[300.3, 200.7], [100.1, 400.9]], np.float32)
+        d = kp[None] - coords[:, None]
+        ang = np.arctan2(d[..., 1], d[..., 0]) + rng.normal(0, 0.1, (tn, vn))
+        direct = np.stack([np.cos(ang), np.sin(ang)], -1).astype(np.float32) * rng.uniform(0.5, 2, (tn, vn, 1)).astype(np.float32)
+        hyp = (kp[None] + rng.normal(0, 20, (hn, vn, 2))).astype(np.float32)
+        ref = np.zeros((hn, vn, tn), np.uint8)
+        O.voting_for_hypothesis(direct, coords, hyp, ref, 0.99)
+        out = torch.full(ref.shape, 9, dtype=torch.uint8, device=device)
+        rv.voting_for_hypothesis_dense(cu(direct, device), cu(coords, device), cu(hyp, device), out, 0.99)
+        np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"tn={tn}")
+        cnt = rv.vote_counts(cu(direct, device), cu(coords, device), cu(hyp, device), 0.99).cpu().numpy()
+        np.testing.assert_array_equal(cnt, ref.sum(2), err_msg=f"tn={tn}")

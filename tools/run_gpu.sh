@@ -26,7 +26,10 @@ for s in "$@"; do
     pmcvalu) step pmcvalu 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -T --output-format csv -d "$PWD/gpurun_out/pmc_valu" -o bench -- python3 bench.py --skip-cpu --skip-e2e --steps 20 ;;
     listpmc) step listpmc 300 rocprofv3 -L ;;
     pmcvote) step pmcvote1 600 rocprofv3 --kernel-include-regex k_vote_count --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_INST_CYCLES_SALU -T --output-format csv -d "$PWD/gpurun_out/pmc_vote1" -o v -- python3 bench.py --skip-cpu --skip-e2e --skip-u1 --steps 10 &&
-             step pmcvote2 600 rocprofv3 --kernel-include-regex k_vote_count --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_WAVES SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE SQ_INSTS_VALU_TRANS_F32 -T --output-format csv -d "$PWD/gpurun_out/pmc_vote2" -o v -- python3 bench.py --skip-cpu --skip-e2e --skip-u1 --steps 10 ;;
+             step pmcvote2 600 rocprofv3 --kernel-include-regex k_vote_count --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_WAVES SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE SQ_INSTS_VALU_TRANS_F32 -T --output-format csv -d "$PWD/gpurun_out/pmc_vote2" -o v -- python3 bench.py --skip-cpu --skip-e2e --skip-u1 --steps 10 &&
+             step pmcvote3 600 rocprofv3 --kernel-include-regex k_vote_count --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INST_LEVEL_LDS SQ_ACCUM_PREV_HIRES -T --output-format csv -d "$PWD/gpurun_out/pmc_vote3" -o v -- python3 bench.py --skip-cpu --skip-e2e --skip-u1 --steps 10 ;;
+    pmcbytes) step pmcbytes1 300 rocprofv3 --kernel-include-regex k_vote_bytes --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_INST_CYCLES_SALU -T --output-format csv -d "$PWD/gpurun_out/pmc_bytes1" -o v -- python3 tools/u1_probe.py &&
+              step pmcbytes2 300 rocprofv3 --kernel-include-regex k_vote_bytes --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAVES GRBM_GUI_ACTIVE SQ_INSTS_LDS -T --output-format csv -d "$PWD/gpurun_out/pmc_bytes2" -o v -- python3 tools/u1_probe.py ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

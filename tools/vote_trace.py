@@ -1,0 +1,42 @@
+"""Debug: per-wave start/end timestamps of the pipeline's vote kernel
+(s_memrealtime, 100 MHz) -> when waves start, how long they live, how the
+finish times spread.  GPU only; not part of the product or the tests."""
+import ctypes
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+from pvnet_amd import _lib, synth  # noqa: E402
+from pvnet_amd.ransac_voting_gpu import ransac_voting_layer_v3_from_network  # noqa: E402
+
+L = _lib.load()
+L.pv_debug_set_vote_trace.argtypes = [ctypes.c_void_p]
+f = synth.synthetic_field(1234)
+seg = torch.from_numpy(f["seg"]).cuda()
+vert = torch.from_numpy(f["vertex"]).cuda()
+buf = torch.zeros(16384 * 3, dtype=torch.int64, device="cuda")
+for it in range(4):
+    buf.zero_()
+    L.pv_debug_set_vote_trace(ctypes.c_void_p(buf.data_ptr()) if it else None)
+    ransac_voting_layer_v3_from_network(seg, vert, 512)
+    torch.cuda.synchronize()
+t = buf.view(-1, 3).cpu().numpy()
+t = t[t[:, 0] > 0]
+s, e, hw = t[:, 0], t[:, 1], t[:, 2]
+t0 = s.min()
+s_us, e_us = (s - t0) / 100.0, (e - t0) / 100.0
+life = e_us - s_us
+print("waves", len(t), "span us", e_us.max())
+for name, x in (("start", s_us), ("end", e_us), ("life", life)):
+    q = np.percentile(x, [0, 1, 10, 50, 90, 99, 100])
+    print(f"{name:6s}", " ".join(f"{v:7.2f}" for v in q))
+# per-CU / SE breakdown of the start times (HW_ID: wave[3:0] simd[5:4] cu[11:8] se[14:13] on gfx9)
+cu = (hw >> 8) & 0xF
+se = (hw >> 13) & 0x7
+print("start by SE:", [f"{np.median(s_us[se == k]):.2f}" for k in range(8) if (se == k).any()])
+hist, edges = np.histogram(s_us, bins=20)
+print("start histogram:", hist.tolist(), "edges", np.round(edges[[0, -1]], 2).tolist())
+hist, edges = np.histogram(e_us, bins=20)
+print("end histogram:", hist.tolist(), "edges", np.round(edges[[0, -1]], 2).tolist())
