@@ -40,9 +40,9 @@
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kCompactChunk = 1024;          // pixels per compaction block (256 threads x 4)
+constexpr int kCompactChunk = 256;           // pixels per compaction block (one per thread)
 constexpr int kVoteChunk = 256;              // pixels per LDS-staged sub-chunk of the vote waves
-constexpr int kRefineNJ = 16;                // refine blocks per (image, keypoint)
+constexpr int kRefineNJ = 32;                // refine blocks per (image, keypoint)
 // domain of the fast test's error bound
 constexpr float kHypMax = 1.0e17f;           // |hx|,|hy| above -> exact-only hypothesis
 constexpr float kLattice = 2.5e-6f;          // |h - round(h)| below (both axes) -> exact-only
@@ -166,7 +166,7 @@ __device__ __forceinline__ bool is_fg(const MaskView &m, int b, int r, int c) {
 // --------------------------------------------------------------------------
 struct Workspace {
     int32_t *counts;    // [b][vn][nh]   zeroed by k_fg_count
-    int32_t *ticket;    // [b]           zeroed by k_fg_count
+    int32_t *ticket;    // [b][1 + vn]   zeroed by k_fg_count: per image, per (image, keypoint)
     uint32_t *exotic;   // [b][nchv]     zeroed by k_fg_count (chunk holds a pixel outside the fast domain)
     int64_t nchv;       // vote chunks per image (capacity)
     int64_t zero_words; // counts + ticket + exotic (contiguous)
@@ -180,6 +180,7 @@ struct Workspace {
     int32_t *win;       // [b][vn]
     float *ratio;       // [b][vn]
     double *refpart;    // [b][vn][kRefineNJ][5]
+    double *ksum;       // [b][vn][5]  least-squares sums per keypoint
     size_t total;
 };
 
@@ -191,10 +192,10 @@ Workspace carve(void *base, int b, int H, int W, int vn, int nh) {
     int64_t off = 0;
     auto take = [&](int64_t bytes) { char *q = p ? p + off : nullptr; off = align_up(off + bytes, 256); return q; };
     w.nchv = (P + kVoteChunk - 1) / kVoteChunk;
-    w.zero_words = (int64_t)b * vn * nh + b + b * w.nchv;
+    w.zero_words = (int64_t)b * vn * nh + (int64_t)b * (1 + vn) + b * w.nchv;
     w.counts = (int32_t *)take(4 * w.zero_words);
     w.ticket = w.counts ? w.counts + (int64_t)b * vn * nh : nullptr;
-    w.exotic = w.counts ? (uint32_t *)(w.ticket + b) : nullptr;
+    w.exotic = w.counts ? (uint32_t *)(w.ticket + (int64_t)b * (1 + vn)) : nullptr;
     w.tn = (int32_t *)take(4 * b);
     w.fgtot = (int32_t *)take(4 * b);
     w.blkcnt = (int32_t *)take(4 * b * nblk);
@@ -205,6 +206,7 @@ Workspace carve(void *base, int b, int H, int W, int vn, int nh) {
     w.win = (int32_t *)take(4 * b * vn);
     w.ratio = (float *)take(4 * b * vn);
     w.refpart = (double *)take(8 * 5 * (int64_t)b * vn * kRefineNJ);
+    w.ksum = (double *)take(8 * 5 * (int64_t)b * vn);
     w.total = (size_t)off;
     return w;
 }
@@ -248,7 +250,7 @@ __global__ __launch_bounds__(256) void k_fg_count(MaskView m, int H, int W, int3
 #pragma unroll
     for (int k = 0; k < kCompactChunk / 256; ++k) {
         int64_t p = (int64_t)blk * kCompactChunk + k * 256 + threadIdx.x;
-        f[k] = p < P && is_fg<KIND, EVD>(m, b, (int)(p / W), (int)(p % W));
+        f[k] = p < P && is_fg<KIND, EVD>(m, b, (int)((uint32_t)p / (uint32_t)W), (int)((uint32_t)p % (uint32_t)W));
     }
     int c = 0;
 #pragma unroll
@@ -284,7 +286,7 @@ __global__ __launch_bounds__(256) void k_fg_downsample(MaskView m, int H, int W,
 #pragma unroll
     for (int k = 0; k < kCompactChunk / 256; ++k) {
         int64_t p = (int64_t)blk * kCompactChunk + k * 256 + threadIdx.x;
-        bool f = p < P && is_fg<KIND, EVD>(m, b, (int)(p / W), (int)(p % W));
+        bool f = p < P && is_fg<KIND, EVD>(m, b, (int)((uint32_t)p / (uint32_t)W), (int)((uint32_t)p % (uint32_t)W));
         if (f) f = keep ? keep[b * P + p] != 0 : rand_unit(seed, (uint64_t)b * P + p) < thr;
         c += f;
     }
@@ -298,6 +300,14 @@ __global__ __launch_bounds__(256) void k_fg_downsample(MaskView m, int H, int W,
 // contiguously.  Reads the [b,H,W,vn,2] view through its strides, so the
 // network's NCHW vertex_pred is gathered directly (no permute copy).
 // ==========================================================================
+// debug-only phase stamps (s_memrealtime) of the compaction blocks; see
+// pv_debug_compact_trace
+__device__ uint64_t g_ctrace[4096 * 4];
+__device__ int g_ctrace_on;
+__device__ __forceinline__ void cstamp(int blk, int k) {
+    if (g_ctrace_on && threadIdx.x == 0 && blk < 4096) g_ctrace[blk * 4 + k] = __builtin_amdgcn_s_memrealtime();
+}
+
 struct VertexView {
     const void *p;
     int kind;
@@ -315,7 +325,9 @@ __global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int 
     const int64_t P = (int64_t)H * W;
     __shared__ int sh[8];
     __shared__ int wcnt[K][4];
+    cstamp(blk, 0);
     int2 tot = image_totals(blkcnt + b * nblk, nblk, blk, sh);
+    cstamp(blk, 1);
     const int fgb = tot.x;
     if (fgb < min_num) {
         if (blk == 0 && threadIdx.x == 0) { tn[b] = 0; fgtot[b] = fgb; }
@@ -333,55 +345,79 @@ __global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int 
     }
     const float thr = ds ? (float)max_num / (float)fgb : 0.f;
     const int wid = threadIdx.x / 64;
+    __shared__ int sel[kCompactChunk];   // block-local pixel index of the k-th selected pixel
     bool f[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {        // all mask reads in flight together
+        const int64_t p = (int64_t)blk * kCompactChunk + k * 256 + threadIdx.x;
+        f[k] = p < P && is_fg<KIND, EVD>(m, b, (int)((uint32_t)p / (uint32_t)W), (int)((uint32_t)p % (uint32_t)W));
+    }
     int below[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        int64_t p = (int64_t)blk * kCompactChunk + k * 256 + threadIdx.x;
-        f[k] = p < P && is_fg<KIND, EVD>(m, b, (int)(p / W), (int)(p % W));
+        const int64_t p = (int64_t)blk * kCompactChunk + k * 256 + threadIdx.x;
         if (ds && f[k]) f[k] = keep ? keep[b * P + p] != 0 : rand_unit(seed, (uint64_t)b * P + p) < thr;
-        uint64_t bal = ballot(f[k]);
+        const uint64_t bal = ballot(f[k]);
         below[k] = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
         if (lane_id() == 0) wcnt[k][wid] = __popcll(bal);
     }
     __syncthreads();
-    float4 *eb = pex + (int64_t)b * vn * P;
-    float4 *pb = pix + (int64_t)b * vn * P;
+    int nsel = 0;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        int off = base;
-        for (int q = 0; q < k; ++q) off += wcnt[q][0] + wcnt[q][1] + wcnt[q][2] + wcnt[q][3];
+        int off = nsel;
         for (int q = 0; q < wid; ++q) off += wcnt[k][q];
-        if (f[k]) {
-            int64_t p = (int64_t)blk * kCompactChunk + k * 256 + threadIdx.x;
-            int r = (int)(p / W), c = (int)(p % W);
-            int64_t t = off + below[k];
-            int64_t vo = b * vx.s[0] + r * vx.s[1] + c * vx.s[2];
-            bool exo = false;
-#pragma unroll 3
-            for (int v = 0; v < vn; ++v) {
-                float nx, ny;
+        if (f[k]) sel[off + below[k]] = k * 256 + threadIdx.x;
+        nsel += wcnt[k][0] + wcnt[k][1] + wcnt[k][2] + wcnt[k][3];
+    }
+    __syncthreads();
+    cstamp(blk, 2);
+    // (selected pixel, keypoint) items: consecutive threads take consecutive
+    // pixels of one keypoint, so vertex reads and pex/pix writes coalesce
+    float4 *eb = pex + (int64_t)b * vn * P;
+    float4 *pb = pix + (int64_t)b * vn * P;
+    const int nitem = nsel * vn;
+    constexpr int U = 4;                 // items per thread in flight
+    for (int it0 = threadIdx.x; it0 < nitem; it0 += 256 * U) {
+        float nx[U], ny[U];
+        int vv[U], kk[U], rr[U], cc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int it = it0 + 256 * u;
+            nx[u] = ny[u] = 0.f;
+            vv[u] = -1;
+            if (it < nitem) {
+                const int v = it / nsel, k = it - v * nsel;
+                const uint32_t p = (uint32_t)blk * kCompactChunk + sel[k];   // H, W <= 65535: fits
+                const int r = (int)(p / (uint32_t)W), c = (int)(p - (uint32_t)r * W);
+                const int64_t vo = b * vx.s[0] + r * vx.s[1] + c * vx.s[2] + v * vx.s[3];
                 if (vx.kind == PV_VERTEX_F32) {
-                    const float *q = (const float *)vx.p + vo;
-                    nx = q[v * vx.s[3]];
-                    ny = q[v * vx.s[3] + vx.s[4]];
+                    nx[u] = ((const float *)vx.p)[vo];
+                    ny[u] = ((const float *)vx.p)[vo + vx.s[4]];
                 } else {
-                    const __half *q = (const __half *)vx.p + vo;
-                    nx = __half2float(q[v * vx.s[3]]);
-                    ny = __half2float(q[v * vx.s[3] + vx.s[4]]);
+                    nx[u] = __half2float(((const __half *)vx.p)[vo]);
+                    ny[u] = __half2float(((const __half *)vx.p)[vo + vx.s[4]]);
                 }
-                eb[(int64_t)v * P + t] = make_float4((float)c, (float)r, nx, ny);
-                // fast-test data: exact norm1 validity (KU:119-121), unit direction via fp64
-                float n1 = sqrtf(nx * nx + ny * ny);
-                bool valid = !((double)n1 < 1e-6);
-                exo |= valid && !(n1 <= kN1Max);
-                double N = sqrt((double)nx * nx + (double)ny * ny);
-                pb[(int64_t)v * P + t] = make_float4(valid ? (float)c : __builtin_nanf(""), (float)r,
-                                                     (float)(nx / N), (float)(ny / N));
+                vv[u] = v; kk[u] = k; rr[u] = r; cc[u] = c;
             }
-            if (exo) atomicOr(&exotic[b * nchv + t / kVoteChunk], 1u);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (vv[u] < 0) continue;
+            const int64_t t = base + kk[u];
+            const int64_t o = (int64_t)vv[u] * P + t;
+            eb[o] = make_float4((float)cc[u], (float)rr[u], nx[u], ny[u]);
+            // fast-test data: exact norm1 validity (KU:119-121); the direction
+            // rounded per component (any positive scale: rsq)
+            const float n1 = sqrtf(nx[u] * nx[u] + ny[u] * ny[u]);
+            const bool valid = !((double)n1 < 1e-6);
+            const float rs = __builtin_amdgcn_rsqf(fmaf(nx[u], nx[u], ny[u] * ny[u]));
+            pb[o] = make_float4(valid ? (float)cc[u] : __builtin_nanf(""), (float)rr[u], nx[u] * rs, ny[u] * rs);
+            if (valid && !(n1 <= kN1Max)) atomicOr(&exotic[b * nchv + t / kVoteChunk], 1u);
         }
     }
+    __syncthreads();
+    cstamp(blk, 3);
 }
 
 // ==========================================================================
@@ -838,7 +874,8 @@ __device__ __forceinline__ T ld_agent(const T *p) { return __hip_atomic_load(p, 
 __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, const float2 *hyp, const float4 *pex,
                                                       const int32_t *tn, int64_t P, int vn, int nh,
                                                       float thr, int32_t *win_out, float *ratio_out, double *refpart,
-                                                      int32_t *ticket, float confidence, int max_iter, float *out,
+                                                      double *ksum, int32_t *ticket, float confidence, int max_iter,
+                                                      float *out,
                                                       pv_v3_diag diag) {
     const int j = blockIdx.x, v = blockIdx.y, b = blockIdx.z;
     const int n = tn[b];
@@ -886,6 +923,11 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
         if (lane_id() == 0) sacc[threadIdx.x / 64][k] = s;
     }
     __syncthreads();
+    // Two-level hand-off (a single counter would serialise every block's
+    // atomic at one L2 address): the last of the kRefineNJ blocks of (b, v)
+    // sums their partials, the last keypoint of image b solves.
+    int32_t *tk_img = ticket + (int64_t)b * (1 + vn);
+    int32_t *tk_v = tk_img + 1 + v;
     if (threadIdx.x < 64) {   // wave 0: publish this block's partials, then take a ticket
         const int k = threadIdx.x;
         double *rp = refpart + (((int64_t)b * vn + v) * kRefineNJ + j) * 5;
@@ -896,23 +938,39 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         int t = 0;
-        if (k == 0) t = __hip_atomic_fetch_add(&ticket[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == 0) t = __hip_atomic_fetch_add(tk_v, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         t = __shfl(t, 0);
-        if (k == 0) slast = (t == kRefineNJ * vn - 1);
+        if (k == 0) slast = (t == kRefineNJ - 1);
     }
     __syncthreads();
     if (!slast || threadIdx.x >= 64) return;
-    // ---- last block of image b: solve for every keypoint (lane = keypoint) ----
+    // ---- last block of (b, v): sum the keypoint's partials (lane = (jj, k)) ----
+    {
+        const int k = threadIdx.x;
+        const double *rp = refpart + ((int64_t)b * vn + v) * kRefineNJ * 5;
+        double s5[5] = {0, 0, 0, 0, 0};
+        for (int jj = k; jj < kRefineNJ; jj += 64)
+#pragma unroll
+            for (int q = 0; q < 5; ++q) s5[q] += ld_agent(&rp[jj * 5 + q]);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) s5[q] = wave_sum_d(s5[q]);
+        double *ks = ksum + ((int64_t)b * vn + v) * 5;
+        if (k < 5) st_agent(&ks[k], k == 0 ? s5[0] : k == 1 ? s5[1] : k == 2 ? s5[2] : k == 3 ? s5[3] : s5[4]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int t = 0;
+        if (k == 0) t = __hip_atomic_fetch_add(tk_img, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = __shfl(t, 0);
+        if (t != vn - 1) return;
+    }
+    // ---- last keypoint of image b: solve for every keypoint (lane = keypoint) ----
     const int vv = threadIdx.x;
     const bool act = vv < vn;
     float A00 = 0, A01 = 0, A11 = 0, B0 = 0, B1 = 0, rat = 3.0e38f;
     int wi = 0;
     if (act) {
-        double s[5] = {0, 0, 0, 0, 0};
-        const double *rp = refpart + ((int64_t)b * vn + vv) * kRefineNJ * 5;
-        for (int jj = 0; jj < kRefineNJ; ++jj)
-            for (int k = 0; k < 5; ++k) s[k] += ld_agent(&rp[jj * 5 + k]);
-        A00 = (float)s[0]; A01 = (float)s[1]; A11 = (float)s[2]; B0 = (float)s[3]; B1 = (float)s[4];
+        const double *ks = ksum + ((int64_t)b * vn + vv) * 5;
+        A00 = (float)ld_agent(&ks[0]); A01 = (float)ld_agent(&ks[1]); A11 = (float)ld_agent(&ks[2]);
+        B0 = (float)ld_agent(&ks[3]); B1 = (float)ld_agent(&ks[4]);
         rat = ld_agent(&ratio_out[b * vn + vv]);
         wi = ld_agent(&win_out[b * vn + vv]);
     }
@@ -1773,6 +1831,10 @@ int pv_vote_counts(const float *direct, const float *coords, const float *hypo, 
 
 // debug only (not in pvvote.h): per-wave timestamps of the next pipeline vote launches
 void pv_debug_set_vote_trace(uint64_t *buf) { g_vote_trace = buf; }
+int pv_debug_compact_trace(int on, uint64_t *host, int n) {
+    if (host) return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ctrace), sizeof(uint64_t) * (size_t)n);
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_ctrace_on), &on, sizeof(int));
+}
 
 size_t pv_v3_workspace_size(int32_t b, int32_t H, int32_t W, int32_t vn, int32_t n_hyp) {
     if (b <= 0 || H <= 0 || W <= 0 || vn <= 0 || n_hyp <= 0) return 0;
@@ -1794,7 +1856,8 @@ int pv_ransac_voting_v3(const pv_image_desc *img, const pv_vote_params *prm, flo
     const int b = img->b, vn = img->vn;
     const int64_t P = (int64_t)img->H * img->W;
     k_refine_solve<<<dim3(kRefineNJ, vn, b), 256, 0, s>>>(w.counts, w.hyp, w.pex, w.tn, P, vn, nh,
-                                                          prm->inlier_thresh, w.win, w.ratio, w.refpart, w.ticket,
+                                                          prm->inlier_thresh, w.win, w.ratio, w.refpart, w.ksum,
+                                                          w.ticket,
                                                           prm->confidence, prm->max_iter, out, dg);
     if ((r = last())) return r;
     if (dg.counts) {
