@@ -1,0 +1,65 @@
+"""World-size-2 stream over gloo on CPU: round-robin sharding and the single
+result gather of pvnet_amd.distributed, with the oracle's v3 standing in for
+the device layer (the product path itself needs a GPU)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from pvnet_amd import distributed as D
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _field(i):
+    """Small synthetic field for image i: 48x64, 3 keypoints."""
+    rng = np.random.default_rng(100 + i)
+    H, W, vn = 48, 64, 3
+    yy, xx = np.mgrid[0:H, 0:W]
+    mask = ((xx - 32) ** 2 + (yy - 24) ** 2 < (12 + i) ** 2).astype(np.int64)
+    kp = rng.uniform([20, 14], [44, 34], (vn, 2)).astype(np.float32)
+    d = kp[None, None] - np.stack([xx, yy], -1)[:, :, None].astype(np.float32)
+    ang = np.arctan2(d[..., 1], d[..., 0]) + rng.normal(0, 0.05, (H, W, vn))
+    vertex = np.stack([np.cos(ang), np.sin(ang)], -1).astype(np.float32) * mask[..., None, None]
+    return torch.from_numpy(mask[None]), torch.from_numpy(vertex[None])
+
+
+def _oracle_vote(mask, vertex):
+    from oracle import oracle as O
+    kp = O.ransac_voting_layer_v3(mask.numpy(), vertex.numpy(), 32, min_num=10, seed=0)
+    return torch.from_numpy(np.asarray(kp, np.float32))
+
+
+def _worker(rank, world, port, n_images, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = D.run_stream(_field, _oracle_vote, n_images, rank, world, (3, 2), torch.device("cpu"))
+        if rank == 0:
+            np.save(out_path, res.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_round_robin():
+    assert D.shard(5, 0, 2) == [0, 2, 4] and D.shard(5, 1, 2) == [1, 3]
+    assert D.shard(1, 1, 2) == []
+    with pytest.raises(ValueError):
+        D.shard(4, 2, 2)
+
+
+@pytest.mark.parametrize("n_images", [5, 1])
+def test_stream_world2_gloo(tmp_path, n_images):
+    out = str(tmp_path / "res.npy")
+    mp.spawn(_worker, args=(2, _free_port(), n_images, out), nprocs=2, join=True)
+    got = np.load(out)
+    want = np.stack([_oracle_vote(*_field(i)).numpy().reshape(3, 2) for i in range(n_images)])
+    np.testing.assert_array_equal(got, want)

@@ -19,6 +19,7 @@ for s in "$@"; do
     testsall) step gpu_tests 900 python -m pytest tests -m gpu -q ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
+    benchfull) step bench 600 python bench.py && cp gpurun_out/bench.log gpurun_out/bench_full.log ;;
     benchquick) step bench 400 python bench.py --steps 20 --warmup 5 --skip-cpu ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$PWD/gpurun_out/prof" -o bench -- python3 bench.py --skip-cpu --skip-e2e ;;
     pmcfetch) step pmcfetch 600 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d "$PWD/gpurun_out/pmc_fetch" -o bench -- python3 bench.py --skip-cpu --skip-e2e --steps 20 ;;
