@@ -11,8 +11,11 @@
  *   - Every pointer is a DEVICE pointer (hipMalloc / torch CUDA tensor memory)
  *     unless the comment says otherwise.  Sizes are element counts.
  *   - Every call is asynchronous on `stream` (a hipStream_t; NULL = the null
- *     stream) and performs no allocation and no host synchronisation, so the
- *     calls can be captured into a hipGraph.
+ *     stream) and performs no host synchronisation, so the calls can be
+ *     captured into a hipGraph.  The pipelines allocate nothing (caller
+ *     workspace); pv_voting_for_hypothesis, whose reference signature has no
+ *     workspace, takes its operand scratch with stream-ordered
+ *     hipMallocAsync / hipFreeAsync on `stream`.
  *   - Return value: 0 on success; a positive hipError_t from the launch; or a
  *     negative PV_E* code for a bad argument.  Nothing ever calls exit()
  *     (the reference's gpuAssert does, cuda_common.h:19-26).
