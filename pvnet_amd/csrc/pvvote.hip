@@ -585,8 +585,18 @@ struct ExactSlab<false> {
 
 template <bool GEN, bool PREPPED>
 __device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, ExactSlab<PREPPED> &stagex, int b, int v, int hg, int ts,
-                                             int te, int n) {
+                                             int te, int n, int64_t rem_after, int64_t wave_total, int &nfix) {
     const int lane = lane_id();
+    // Issue priority from the work this wave still has (0..3): the SIMD's
+    // arbiter otherwise favours the oldest wave, so equal shares finish
+    // staggered and the last waves run alone; this keeps them level.
+    auto set_prio = [&](int64_t remaining) {
+        const int64_t q = remaining * 4 / (wave_total + 1);
+        if (q >= 3) __builtin_amdgcn_s_setprio(3);
+        else if (q == 2) __builtin_amdgcn_s_setprio(2);
+        else if (q == 1) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+    };
     const float tau = a.tau;
     constexpr float kBig = 3.0e38f;
 
@@ -696,7 +706,10 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, Exact
                 const float ay = fmaxf(fabsf(hy[i] - yn), fabsf(hy[i] - yx));
                 const float D = fmaf(__builtin_amdgcn_sqrtf(fmaf(ax, ax, ay * ay)), 1.00001f, Bv[i] * 1e-6f);
                 const float g = fmaf(a.gzr, D, a.gzf * Bv[i]);
-                gd[i] = g >= 0.f ? g : __builtin_inff();
+                // a hypothesis outside the fast test (hx, hy NaN -> g NaN) gets
+                // -1: its z is NaN, never counted, and it must never trigger
+                // the band (the exact-only loop below decides it)
+                gd[i] = g >= 0.f ? g : -1.f;
             }
         };
         if (!slow) {
@@ -739,7 +752,10 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, Exact
                 z = zval(q2, hx[1], hy[1]); cnt[1] += z > gd[1]; m1 = fminf(m1, fabsf(z));
                 z = zval(q3, hx[0], hy[0]); cnt[0] += z > gd[0]; m0 = fminf(m0, fabsf(z));
                 z = zval(q3, hx[1], hy[1]); cnt[1] += z > gd[1]; m1 = fminf(m1, fabsf(z));
-                if (__builtin_amdgcn_ballot_w64(m0 <= gd[0] || m1 <= gd[1])) fix_step(j);
+                if (__builtin_amdgcn_ballot_w64(m0 <= gd[0] || m1 <= gd[1])) {
+                    ++nfix;
+                    fix_step(j);
+                }
             };
             static_assert(kHypLane == 2, "step() is written for two hypotheses per lane");
             // the slab past np holds NaN pixels (never counted, never in the
@@ -748,7 +764,10 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, Exact
             F4 a0 = stage[0], a1 = stage[1], a2 = stage[2], a3 = stage[3];
             for (int it = 0; it < nit; ++it) {
                 const int j = it * 8;
-                if ((j & (kWave - 1)) == 0) set_band(j / kWave);
+                if ((j & (kWave - 1)) == 0) {
+                    set_band(j / kWave);
+                    set_prio(rem_after + (te - s0 - j));
+                }
                 const F4 b0 = stage[j + 4], b1 = stage[j + 5], b2 = stage[j + 6], b3 = stage[j + 7];
                 step(a0, a1, a2, a3, j);
                 const int jn = (j + 8) & (kVoteChunk - 1);
@@ -812,6 +831,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     int64_t total = 0;
     for (int b = 0; b < a.b; ++b) total += (int64_t)a.vn * a.hgn * (a.tn_dev ? a.tn_dev[b] : a.tn_host);
     int64_t lo = total * wave / nwaves, hi = total * (wave + 1) / nwaves;
+    const int64_t wave_total = hi - lo;
+    int nfix = 0, nseg = 0;   // diagnostics (trace)
     // walk the segments of [lo, hi)
     int b = 0;
     int64_t base = 0;
@@ -825,15 +846,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         int te = (int)min<int64_t>((int64_t)n, ts + (hi - lo));
         int v = g / a.hgn, hg = g % a.hgn;
         vote_segment<GEN, PREPPED>(a, stage, stagex, uniform(b), uniform(v), uniform(hg), uniform(ts), uniform(te),
-                                   n);
+                                   n, hi - lo - (te - ts), wave_total, nfix);
         lo += te - ts;
+        ++nseg;
     }
     if (a.trace && lane_id() == 0) {
         uint32_t hw;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        a.trace[wave * 3] = t_start;
-        a.trace[wave * 3 + 1] = __builtin_amdgcn_s_memrealtime();
-        a.trace[wave * 3 + 2] = hw;
+        a.trace[wave * 4] = t_start;
+        a.trace[wave * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+        a.trace[wave * 4 + 2] = hw;
+        a.trace[wave * 4 + 3] = ((uint64_t)nseg << 32) | (uint32_t)nfix;
     }
 }
 

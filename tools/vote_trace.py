@@ -16,15 +16,16 @@ L.pv_debug_set_vote_trace.argtypes = [ctypes.c_void_p]
 f = synth.synthetic_field(1234)
 seg = torch.from_numpy(f["seg"]).cuda()
 vert = torch.from_numpy(f["vertex"]).cuda()
-buf = torch.zeros(16384 * 3, dtype=torch.int64, device="cuda")
+buf = torch.zeros(16384 * 4, dtype=torch.int64, device="cuda")
 for it in range(4):
     buf.zero_()
     L.pv_debug_set_vote_trace(ctypes.c_void_p(buf.data_ptr()) if it else None)
     ransac_voting_layer_v3_from_network(seg, vert, 512)
     torch.cuda.synchronize()
-t = buf.view(-1, 3).cpu().numpy()
+t = buf.view(-1, 4).cpu().numpy()
 t = t[t[:, 0] > 0]
 s, e, hw = t[:, 0], t[:, 1], t[:, 2]
+nfix, nseg = t[:, 3] & 0xffffffff, t[:, 3] >> 32
 t0 = s.min()
 s_us, e_us = (s - t0) / 100.0, (e - t0) / 100.0
 life = e_us - s_us
@@ -40,3 +41,16 @@ hist, edges = np.histogram(s_us, bins=20)
 print("start histogram:", hist.tolist(), "edges", np.round(edges[[0, -1]], 2).tolist())
 hist, edges = np.histogram(e_us, bins=20)
 print("end histogram:", hist.tolist(), "edges", np.round(edges[[0, -1]], 2).tolist())
+
+life = e_us - s_us
+for name, m in (("1 segment", nseg == 1), ("2 segments", nseg == 2), ("3+ segments", nseg >= 3)):
+    if m.any():
+        print(f"{name:12s} waves {m.sum():5d}  life median {np.median(life[m]):6.2f}  max {life[m].max():6.2f}")
+print("fix steps per wave: median", np.median(nfix), "p90", np.percentile(nfix, 90), "max", nfix.max())
+order = np.argsort(life)
+for q in (0.1, 0.5, 0.9, 0.99):
+    k = order[int(q * (len(order) - 1))]
+    print(f"life q{q}: {life[k]:.2f} us nfix {nfix[k]} nseg {nseg[k]}")
+top = order[-50:]
+print("slowest 50: nfix mean", nfix[top].mean(), "nseg mean", nseg[top].mean(), " | all: nfix mean", nfix.mean(), "nseg mean", nseg.mean())
+print("corr(life, nfix)", np.corrcoef(life, nfix)[0, 1], "corr(life, nseg)", np.corrcoef(life, nseg)[0, 1])
