@@ -168,12 +168,12 @@ struct Workspace {
     int32_t *counts;    // [b][vn][nh]   zeroed by k_fg_count
     int32_t *ticket;    // [b][1 + vn]   zeroed by k_fg_count: per image, per (image, keypoint)
     uint32_t *exotic;   // [b][nchv]     zeroed by k_fg_count (chunk holds a pixel outside the fast domain)
+    int32_t *dsagg;     // [b][nblk]     zeroed by k_fg_count: downsampled count + 1 per block (look-back)
     int64_t nchv;       // vote chunks per image (capacity)
-    int64_t zero_words; // counts + ticket + exotic (contiguous)
+    int64_t zero_words; // counts + ticket + exotic + dsagg (contiguous)
     int32_t *tn;        // [b] compacted pixels (0 = image skipped)
     int32_t *fgtot;     // [b] foreground before downsampling
     int32_t *blkcnt;    // [b][nblk]
-    int32_t *dscnt;     // [b][nblk]
     float4 *pex;        // [b][vn][P]   exact pixel data (cx, cy, nx, ny): reference operands
     float4 *pix;        // [b][vn][P]   fast-test data (fx, cy, ux, uy)
     float2 *hyp;        // [b][nh][vn]  (reference layout)
@@ -192,14 +192,14 @@ Workspace carve(void *base, int b, int H, int W, int vn, int nh) {
     int64_t off = 0;
     auto take = [&](int64_t bytes) { char *q = p ? p + off : nullptr; off = align_up(off + bytes, 256); return q; };
     w.nchv = (P + kVoteChunk - 1) / kVoteChunk;
-    w.zero_words = (int64_t)b * vn * nh + (int64_t)b * (1 + vn) + b * w.nchv;
+    w.zero_words = (int64_t)b * vn * nh + (int64_t)b * (1 + vn) + b * w.nchv + b * nblk;
     w.counts = (int32_t *)take(4 * w.zero_words);
     w.ticket = w.counts ? w.counts + (int64_t)b * vn * nh : nullptr;
     w.exotic = w.counts ? (uint32_t *)(w.ticket + (int64_t)b * (1 + vn)) : nullptr;
+    w.dsagg = w.counts ? (int32_t *)(w.exotic + b * w.nchv) : nullptr;
     w.tn = (int32_t *)take(4 * b);
     w.fgtot = (int32_t *)take(4 * b);
     w.blkcnt = (int32_t *)take(4 * b * nblk);
-    w.dscnt = (int32_t *)take(4 * b * nblk);
     w.pex = (float4 *)take(16 * b * vn * P);
     w.pix = (float4 *)take(16 * b * vn * P);
     w.hyp = (float2 *)take(8 * (int64_t)b * nh * vn);
@@ -210,6 +210,12 @@ Workspace carve(void *base, int b, int H, int W, int vn, int nh) {
     w.total = (size_t)off;
     return w;
 }
+
+// agent-scope (device-wide) relaxed atomics for the in-kernel hand-offs
+template <typename T>
+__device__ __forceinline__ void st_agent(T *p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 // --------------------------------------------------------------------------
 // block helpers (256 threads = 4 waves)
@@ -270,30 +276,6 @@ __device__ __forceinline__ int2 image_totals(const int32_t *cnt, int nblk, int u
     return block_sum2(all, pre, sh);
 }
 
-// K1b: recount with the Bernoulli(max_num/fg) selection (RV:543-546, RV:351-355);
-// exits at once for images that need none (the common case).
-template <int KIND, bool EVD>
-__global__ __launch_bounds__(256) void k_fg_downsample(MaskView m, int H, int W, const int32_t *blkcnt,
-                                                       int32_t *dscnt, int nblk, int min_num, int max_num,
-                                                       uint64_t seed, const uint8_t *keep) {
-    const int b = blockIdx.y, blk = blockIdx.x;
-    __shared__ int sh[8];
-    const int fgb = image_totals(blkcnt + b * nblk, nblk, 0, sh).x;
-    if (fgb < min_num || fgb <= max_num) return;
-    const int64_t P = (int64_t)H * W;
-    const float thr = (float)max_num / (float)fgb;
-    int c = 0;
-#pragma unroll
-    for (int k = 0; k < kCompactChunk / 256; ++k) {
-        int64_t p = (int64_t)blk * kCompactChunk + k * 256 + threadIdx.x;
-        bool f = p < P && is_fg<KIND, EVD>(m, b, (int)((uint32_t)p / (uint32_t)W), (int)((uint32_t)p % (uint32_t)W));
-        if (f) f = keep ? keep[b * P + p] != 0 : rand_unit(seed, (uint64_t)b * P + p) < thr;
-        c += f;
-    }
-    int2 t = block_sum2(c, 0, sh);
-    if (threadIdx.x == 0) dscnt[b * nblk + blk] = t.x;
-}
-
 // ==========================================================================
 // K2: row-major stream compaction (RV:548-552): coords (x=col, y=row) and the
 // per-keypoint raw directions, keypoint-major so the vote waves read them
@@ -316,7 +298,7 @@ struct VertexView {
 
 template <int KIND, bool EVD>
 __global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int H, int W, int vn,
-                                                 const int32_t *blkcnt, const int32_t *dscnt, int nblk, int min_num,
+                                                 const int32_t *blkcnt, int32_t *dsagg, int nblk, int min_num,
                                                  int max_num, uint64_t seed, const uint8_t *keep, int32_t *tn,
                                                  int32_t *fgtot, float4 *pex, float4 *pix, uint32_t *exotic,
                                                  int64_t nchv) {
@@ -335,11 +317,7 @@ __global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int 
     }
     const bool ds = fgb > max_num;
     int base = tot.y;
-    if (ds) {
-        int2 d = image_totals(dscnt + b * nblk, nblk, blk, sh);
-        base = d.y;
-        if (blk == 0 && threadIdx.x == 0) { tn[b] = d.x; fgtot[b] = fgb; }
-    } else if (blk == 0 && threadIdx.x == 0) {
+    if (!ds && blk == 0 && threadIdx.x == 0) {
         tn[b] = fgb;
         fgtot[b] = fgb;
     }
@@ -369,6 +347,25 @@ __global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int 
         for (int q = 0; q < wid; ++q) off += wcnt[k][q];
         if (f[k]) sel[off + below[k]] = k * 256 + threadIdx.x;
         nsel += wcnt[k][0] + wcnt[k][1] + wcnt[k][2] + wcnt[k][3];
+    }
+    if (ds) {
+        // Downsampled offsets by look-back: publish this block's kept count
+        // (+1, so 0 = not yet; k_fg_count zeroed the array), then add up the
+        // earlier blocks' counts, waiting for each.  Blocks are dispatched in
+        // order, so every block waited on is running or done.
+        int32_t *agg = dsagg + (int64_t)b * nblk;
+        if (threadIdx.x == 0) {
+            st_agent(&agg[blk], nsel + 1);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        int pre = 0;
+        for (int j = threadIdx.x; j < blk; j += 256) {
+            int v;
+            while ((v = ld_agent(&agg[j])) == 0) __builtin_amdgcn_s_sleep(1);
+            pre += v - 1;
+        }
+        base = block_sum2(pre, 0, sh).x;
+        if (blk == nblk - 1 && threadIdx.x == 0) { tn[b] = base + nsel; fgtot[b] = fgb; }
     }
     __syncthreads();
     cstamp(blk, 2);
@@ -724,40 +721,47 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, Exact
             auto fix_step = [&](int j) {
 #pragma unroll 1
                 for (int pi = 0; pi < 4 * kHypLane; ++pi) {
-                    const int p = pi >> 1;
-                    const bool i1 = pi & 1;
-                    const float hxi = i1 ? hx[1] : hx[0], hyi = i1 ? hy[1] : hy[0], gdi = i1 ? gd[1] : gd[0];
+                    const int p = pi / kHypLane, i = pi % kHypLane;
+                    float hxi = hx[0], hyi = hy[0], gdi = gd[0], ex = he[0].x, ey = he[0].y;
+#pragma unroll
+                    for (int k = 1; k < kHypLane; ++k) {
+                        if (i == k) { hxi = hx[k]; hyi = hy[k]; gdi = gd[k]; ex = he[k].x; ey = he[k].y; }
+                    }
                     const bool u = fabsf(zval(stage[j + p], hxi, hyi)) <= gdi;
                     if (__builtin_amdgcn_ballot_w64(u)) {
                         const F4 e = stagex.get(j + p);
-                        const float ex = i1 ? he[1].x : he[0].x, ey = i1 ? he[1].y : he[0].y;
                         const int r = (u && exact_vote(e.z, e.w, e.x, e.y, ex, ey, a.thr)) ? 1 : 0;
-                        cnt[0] += i1 ? 0 : r;
-                        cnt[1] += i1 ? r : 0;
+#pragma unroll
+                        for (int k = 0; k < kHypLane; ++k) cnt[k] += i == k ? r : 0;
                     }
                 }
             };
-            // 4 pixels x 2 hypotheses per step, LDS reads one step ahead into
-            // two named buffers (no register copies).  The band is checked once
-            // per step on min |z| (v_min ignores NaN, so invalid pixels and
-            // non-fast hypotheses never trigger it).
+            // 4 pixels x kHypLane hypotheses per step, LDS reads one step ahead
+            // into two named buffers (no register copies).  The band is checked
+            // once per step on min |z| per hypothesis (v_min ignores NaN, so
+            // invalid pixels and non-fast hypotheses never trigger it).
             auto step = [&](F4 q0, F4 q1, F4 q2, F4 q3, int j) {
-                float m0 = kBig, m1 = kBig;
-                float z;
-                z = zval(q0, hx[0], hy[0]); cnt[0] += z > gd[0]; m0 = fminf(m0, fabsf(z));
-                z = zval(q0, hx[1], hy[1]); cnt[1] += z > gd[1]; m1 = fminf(m1, fabsf(z));
-                z = zval(q1, hx[0], hy[0]); cnt[0] += z > gd[0]; m0 = fminf(m0, fabsf(z));
-                z = zval(q1, hx[1], hy[1]); cnt[1] += z > gd[1]; m1 = fminf(m1, fabsf(z));
-                z = zval(q2, hx[0], hy[0]); cnt[0] += z > gd[0]; m0 = fminf(m0, fabsf(z));
-                z = zval(q2, hx[1], hy[1]); cnt[1] += z > gd[1]; m1 = fminf(m1, fabsf(z));
-                z = zval(q3, hx[0], hy[0]); cnt[0] += z > gd[0]; m0 = fminf(m0, fabsf(z));
-                z = zval(q3, hx[1], hy[1]); cnt[1] += z > gd[1]; m1 = fminf(m1, fabsf(z));
-                if (__builtin_amdgcn_ballot_w64(m0 <= gd[0] || m1 <= gd[1])) {
+                float m[kHypLane];
+#pragma unroll
+                for (int i = 0; i < kHypLane; ++i) m[i] = kBig;
+                const F4 *qs[4] = {&q0, &q1, &q2, &q3};
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+#pragma unroll
+                    for (int i = 0; i < kHypLane; ++i) {
+                        const float z = zval(*qs[p], hx[i], hy[i]);
+                        cnt[i] += z > gd[i];
+                        m[i] = fminf(m[i], fabsf(z));
+                    }
+                }
+                bool hit = false;
+#pragma unroll
+                for (int i = 0; i < kHypLane; ++i) hit |= m[i] <= gd[i];
+                if (__builtin_amdgcn_ballot_w64(hit)) {
                     ++nfix;
                     fix_step(j);
                 }
             };
-            static_assert(kHypLane == 2, "step() is written for two hypotheses per lane");
             // the slab past np holds NaN pixels (never counted, never in the
             // band), so the loop runs whole 8-pixel iterations
             const int nit = (np + 7) >> 3;
@@ -880,10 +884,6 @@ __device__ inline bool lu2_inv(float a00, float a01, float a10, float a11, float
     return true;
 }
 
-template <typename T>
-__device__ __forceinline__ void st_agent(T *p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-template <typename T>
-__device__ __forceinline__ T ld_agent(const T *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 // ==========================================================================
 // K6: winner per (image, keypoint) (RV:567-575) + least-squares partial sums
@@ -1675,9 +1675,7 @@ struct CompactStage {
         dim3 grid(a->nblk, a->b);
         k_fg_count<KIND, EVD><<<grid, 256, 0, a->s>>>(a->m, a->H, a->W, a->ws.blkcnt, a->nblk, a->ws.counts,
                                                       a->ws.zero_words);
-        k_fg_downsample<KIND, EVD><<<grid, 256, 0, a->s>>>(a->m, a->H, a->W, a->ws.blkcnt, a->ws.dscnt, a->nblk,
-                                                           a->min_num, a->max_num, a->seed, a->keep);
-        k_compact<KIND, EVD><<<grid, 256, 0, a->s>>>(a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.dscnt,
+        k_compact<KIND, EVD><<<grid, 256, 0, a->s>>>(a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.dsagg,
                                                      a->nblk, a->min_num, a->max_num, a->seed, a->keep, a->ws.tn,
                                                      a->ws.fgtot, a->ws.pex, a->ws.pix, a->ws.exotic, a->ws.nchv);
         return last();
