@@ -217,6 +217,38 @@ def measure_u1(dev, hn=512, reps=20):
                 frac=nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, hn=hn, tn=tn)
 
 
+def measure_batch(dev, b=32, hn=512, steps=10):
+    """configs[2]-shaped voting throughput: one call votes a batch of 32
+    fields whose foreground spans ~2k..30k pixels (13 disk radii, cycling),
+    captured as a hipGraph of `steps` calls; voting only (fp32)."""
+    from pvnet_amd import ransac_voting_gpu as rvg
+    from pvnet_amd import synth
+    fs = [synth.synthetic_field(5000 + i, radius=25.0 + 72.5 * (i % 13) / 12.0) for i in range(b)]
+    seg = torch.from_numpy(np.concatenate([f["seg"] for f in fs])).to(dev)
+    ver = torch.from_numpy(np.concatenate([f["vertex"] for f in fs])).to(dev)
+    work = rvg.VotingWorkspace()
+    out = torch.zeros((steps, b, VN, 2), dtype=torch.float32, device=dev)
+    s = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(s):
+        for k in range(3):
+            rvg.ransac_voting_layer_v3_from_network(seg, ver, hn, _seed=k, _workspace=work, out=out[0])
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for k in range(steps):
+                rvg.ransac_voting_layer_v3_from_network(seg, ver, hn, _seed=100 + k, _workspace=work, out=out[k])
+    g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    g.replay()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    err = float(np.abs(out.cpu().numpy() - np.stack([f["keypoints"] for f in fs])[None]).max())
+    return dict(images_per_s=round(b * steps / dt, 1), ms_per_batch=round(dt / steps * 1e3, 4), batch=b,
+                tn_range=[min(f["tn"] for f in fs), max(f["tn"] for f in fs)], max_kp_err_px=round(err, 4))
+
+
 def measure_e2e(dev, seg_dtype=torch.float32, iters=10):
     """configs[1]: ResNet-18 seg+vector-field forward (PyTorch-ROCm, MIOpen) +
     the HIP v3 layer on one 480x640 image, eager, random-init weights."""
@@ -325,6 +357,10 @@ def report(args, ws, res, final_err, seg, ver, fb, rvg, work, dev):
             line["e2e_config1"] = measure_e2e(dev)
         except Exception as e:
             line["e2e_config1"] = {"error": repr(e)}
+        try:
+            line["voting_config2_batch32"] = measure_batch(dev)
+        except Exception as e:
+            line["voting_config2_batch32"] = {"error": repr(e)}
     if ws == 1 and not args.skip_cpu:
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     print(json.dumps(line), flush=True)

@@ -905,6 +905,16 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
     __shared__ uint64_t skey[4];
     __shared__ double sacc[4][5];
     __shared__ int slast;
+    // this block's pixels, loaded before the argmax so both latencies overlap
+    constexpr int U = 4;
+    const float4 *eb = pex + ((int64_t)b * vn + v) * P;
+    const int t0 = j * 256 + threadIdx.x, tstep = kRefineNJ * 256;
+    float4 e[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int t = t0 + u * tstep;
+        e[u] = t < n ? eb[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     // argmax over h, first index on ties: key = count << 32 | ~h
     uint64_t key = 0;
     const int32_t *cnt = counts + ((int64_t)b * vn + v) * nh;
@@ -927,19 +937,21 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
     float2 best = make_float2(0.f, 0.f);
     if (n > 0 && 0.f < ratio) best = hyp[((int64_t)b * nh + win) * vn + v];
     double acc[5] = {0, 0, 0, 0, 0};
-    const float4 *eb = pex + ((int64_t)b * vn + v) * P;
-    for (int t = j * 256 + threadIdx.x; t < n; t += kRefineNJ * 256) {
-        const float4 e = eb[t];   // (cx, cy, nx, ny)
-        if (exact_vote(e.z, e.w, e.x, e.y, best.x, best.y, thr)) {
-            float n0 = e.w, n1 = -e.z;                  // RV:585-587 normal = (d_y, -d_x)
-            float bb = n0 * e.x + n1 * e.y;             // RV:597 (2-term fp32 sum)
+    auto accum = [&](const float4 &q) {   // (cx, cy, nx, ny)
+        if (exact_vote(q.z, q.w, q.x, q.y, best.x, best.y, thr)) {
+            float n0 = q.w, n1 = -q.z;                  // RV:585-587 normal = (d_y, -d_x)
+            float bb = n0 * q.x + n1 * q.y;             // RV:597 (2-term fp32 sum)
             acc[0] += (double)n0 * n0;
             acc[1] += (double)n0 * n1;
             acc[2] += (double)n1 * n1;
             acc[3] += (double)n0 * bb;
             acc[4] += (double)n1 * bb;
         }
-    }
+    };
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (t0 + u * tstep < n) accum(e[u]);
+    for (int t = t0 + U * tstep; t < n; t += tstep) accum(eb[t]);   // images larger than U * tstep
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
         double s = wave_sum_d(acc[k]);
