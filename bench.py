@@ -249,31 +249,47 @@ def measure_batch(dev, b=32, hn=512, steps=10):
                 tn_range=[min(f["tn"] for f in fs), max(f["tn"] for f in fs)], max_kp_err_px=round(err, 4))
 
 
-def measure_e2e(dev, seg_dtype=torch.float32, iters=10):
-    """configs[1]: ResNet-18 seg+vector-field forward (PyTorch-ROCm, MIOpen) +
-    the HIP v3 layer on one 480x640 image, eager, random-init weights."""
+def measure_e2e(dev, half=False, iters=20):
+    """configs[1] (fp32) / configs[2]'s fp16 backbone: ResNet-18 seg+vector-
+    field forward (PyTorch-ROCm, MIOpen, channels_last) + the HIP v3 layer
+    on one 480x640 image, captured together as one hipGraph; random-init
+    weights (the reference ships none), so the foreground is arbitrary and
+    this times the path, not accuracy."""
     from pvnet_amd import ransac_voting_gpu as rvg
     from pvnet_amd.network import PVNet
+    torch.backends.cudnn.benchmark = True      # MIOpen: search the convolution algorithms once
     torch.manual_seed(0)
-    net = PVNet(18, 2).to(dev).eval().to(memory_format=torch.channels_last)
-    x = torch.randn(1, 3, H, W, device=dev).to(memory_format=torch.channels_last)
+    dt_ = torch.float16 if half else torch.float32
+    net = PVNet(18, 2).to(dev).eval().to(dtype=dt_, memory_format=torch.channels_last)
+    x = torch.randn(1, 3, H, W, device=dev).to(dtype=dt_, memory_format=torch.channels_last)
     ws = rvg.VotingWorkspace()
+    out = torch.zeros((1, VN, 2), dtype=torch.float32, device=dev)
 
     def once():
-        with torch.no_grad(), torch.autocast("cuda", dtype=seg_dtype, enabled=seg_dtype != torch.float32):
-            s, v = net(x)
-        return rvg.ransac_voting_layer_v3_from_network(s.contiguous(), v.contiguous(), 512, _workspace=ws,
-                                                       max_num=30000)
-    for _ in range(3):
-        once()
+        with torch.no_grad():
+            sg, v = net(x)
+        return rvg.ransac_voting_layer_v3_from_network(sg.contiguous(), v.contiguous(), 512, _workspace=ws,
+                                                       max_num=30000, _seed=7, out=out)
+    s = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            once()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            once()
+    g.replay()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(iters):
-        once()
+        g.replay()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / iters
-    return dict(images_per_s=1.0 / dt, ms_per_image=dt * 1e3, backbone_dtype=str(seg_dtype).replace("torch.", ""),
-                note="random-init weights: foreground from an untrained net is arbitrary; timing only")
+    return dict(images_per_s=round(1.0 / dt, 1), ms_per_image=round(dt * 1e3, 4),
+                backbone_dtype="float16" if half else "float32", backbone_gflop=144.9,
+                backbone_tflops=round(144.9e9 / dt / 1e12, 1),
+                note="random-init weights (none ship with the reference): timing only")
 
 
 def cpu_baseline(budget_s):
@@ -357,6 +373,10 @@ def report(args, ws, res, final_err, seg, ver, fb, rvg, work, dev):
             line["e2e_config1"] = measure_e2e(dev)
         except Exception as e:
             line["e2e_config1"] = {"error": repr(e)}
+        try:
+            line["e2e_fp16_backbone"] = measure_e2e(dev, half=True)
+        except Exception as e:
+            line["e2e_fp16_backbone"] = {"error": repr(e)}
         try:
             line["voting_config2_batch32"] = measure_batch(dev)
         except Exception as e:
