@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=1, help="images per GPU per step (configs[1]: batch=1)")
     ap.add_argument("--hn", type=int, default=512, help="round_hyp_num (DEMO:55 / TRAIN:141)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="images in flight: consecutive steps alternate over this many HIP streams (own workspaces)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--skip-e2e", action="store_true")
@@ -96,15 +98,30 @@ def main():
 
     seeds = [rank * 1_000_003 + 17 * k + 3 for k in range(K)]
     s = torch.cuda.Stream(device=dev)
+    NF = max(1, args.inflight)
+    lanes = [torch.cuda.Stream(device=dev) for _ in range(NF)]
+    works = [work] + [rvg.VotingWorkspace() for _ in range(NF - 1)]
 
     def step(k):
-        return rvg.ransac_voting_layer_v3_from_network(seg, ver, args.hn, _seed=seeds[k], _workspace=work,
-                                                       out=out[k])
+        # step k runs on in-flight lane k % NF (its own stream and workspace)
+        with torch.cuda.stream(lanes[k % NF]):
+            return rvg.ransac_voting_layer_v3_from_network(seg, ver, args.hn, _seed=seeds[k],
+                                                           _workspace=works[k % NF], out=out[k])
+
+    def fork():
+        for ln in lanes:
+            ln.wait_stream(torch.cuda.current_stream())
+
+    def join():
+        for ln in lanes:
+            torch.cuda.current_stream().wait_stream(ln)
 
     # warmup (eager; kernels are precompiled, nothing is JIT-compiled)
     with torch.cuda.stream(s):
+        fork()
         for i in range(args.warmup):
             step(i % K)
+        join()
     torch.cuda.synchronize()
 
     graph = None
@@ -112,8 +129,10 @@ def main():
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.stream(s):
             with torch.cuda.graph(graph, stream=s):
+                fork()
                 for k in range(K):
                     step(k)
+                join()
         graph.replay()        # one untimed replay (graph upload)
         torch.cuda.synchronize()
 
@@ -126,8 +145,10 @@ def main():
         if graph is not None:
             graph.replay()
         else:
+            fork()
             for k in range(K):
                 step(k)
+            join()
         if ws > 1:
             dist.all_gather_into_tensor(gathered, out)     # the stream's single keypoint exchange (RCCL)
     torch.cuda.synchronize()
@@ -144,7 +165,20 @@ def main():
     # eager replays of the same K steps (events inside a captured graph do not
     # time the nodes between them)
     vote_ms = time_vote_kernel(rvg, seg, ver, args.hn, seeds, work, out, s)
-    res = dict(elapsed=elapsed, vote_ms=vote_ms, tn=tn)
+    # per-image latency: the same K steps one after another on one stream
+    lat = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(lat, stream=s):
+            for k in range(K):
+                rvg.ransac_voting_layer_v3_from_network(seg, ver, args.hn, _seed=seeds[k], _workspace=work,
+                                                       out=out[k])
+    lat.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lat.replay()
+    torch.cuda.synchronize()
+    latency_ms = (time.perf_counter() - t0) / K * 1e3
+    res = dict(elapsed=elapsed, vote_ms=vote_ms, tn=tn, latency_ms=latency_ms)
     # sanity on the timed outputs
     final_err = float(np.abs(out.cpu().numpy() - fb["keypoints"][None]).max())
     if rank == 0:
@@ -356,12 +390,15 @@ def report(args, ws, res, final_err, seg, ver, fb, rvg, work, dev):
         "dtype": "f32",
         "data": "synthetic S(seed) fields (SURVEY 8(d)): disk r=97.5 -> 29,861 fg px, 9 kp, 0.05 rad noise, "
                 "20% outliers; network layout seg_pred/vertex_pred resident in HBM",
-        "config": {"workload": "LINEMOD-cat-sized frame, batch=%d per GPU: ransac_voting_layer_v3 "
-                               "(hn=%d, thr=0.99) from seg_pred/vertex_pred, hipGraph of %d steps" % (B, args.hn, K),
+        "config": {"workload": "LINEMOD-cat-sized frame, batch=%d per GPU per step: ransac_voting_layer_v3 "
+                               "(hn=%d, thr=0.99) from seg_pred/vertex_pred, hipGraph of %d steps, %d steps in "
+                               "flight on separate streams" % (B, args.hn, K, max(1, args.inflight)),
                    "global_batch": B * ws, "image": [H, W], "keypoints": VN, "round_hyp_num": args.hn,
-                   "foreground_px": int(tn[0]), "parallelism": "dp%d (images sharded, RCCL gather)" % ws},
+                   "foreground_px": int(tn[0]), "parallelism": "dp%d (images sharded, RCCL gather)" % ws,
+                   "images_in_flight": max(1, args.inflight)},
         "roofline": roof,
         "max_kp_err_px": round(final_err, 5),
+        "latency_ms_per_image": round(res["latency_ms"], 5),
     }
     if not args.skip_u1:
         try:
