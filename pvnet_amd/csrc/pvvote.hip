@@ -518,14 +518,27 @@ __device__ __forceinline__ float bcast(float x, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), lane));
 }
 
-__device__ __forceinline__ float wave_min(float x) {
-    for (int o = 32; o > 0; o >>= 1) x = fminf(x, __shfl_xor(x, o));
+// Wave-wide min / max (result in every lane): v_permlane32_swap folds the
+// halves, then xor-swizzles within 32 lanes (no address registers, unlike
+// ds_bpermute).
+template <int XOR>
+__device__ __forceinline__ float swz_xor(float x) {
+    return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x), (XOR << 10) | 0x1f));
+}
+template <bool MAX>
+__device__ __forceinline__ float wave_reduce(float x) {
+    auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : fminf(a, b); };
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(x), __float_as_int(x), false, false);
+    x = op(__int_as_float(r[0]), __int_as_float(r[1]));
+    x = op(x, swz_xor<16>(x));
+    x = op(x, swz_xor<8>(x));
+    x = op(x, swz_xor<4>(x));
+    x = op(x, swz_xor<2>(x));
+    x = op(x, swz_xor<1>(x));
     return x;
 }
-__device__ __forceinline__ float wave_max(float x) {
-    for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
-    return x;
-}
+__device__ __forceinline__ float wave_min(float x) { return wave_reduce<false>(x); }
+__device__ __forceinline__ float wave_max(float x) { return wave_reduce<true>(x); }
 
 // fast data of one pixel from its raw direction (API path without a prepped array)
 __device__ __forceinline__ float4 prep_pixel(float cx, float cy, float nx, float ny) {
