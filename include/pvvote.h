@@ -131,6 +131,13 @@ size_t pv_v3_workspace_size(int32_t b, int32_t H, int32_t W, int32_t vn, int32_t
 int pv_ransac_voting_v3(const pv_image_desc *img, const pv_vote_params *prm, float *out,
                         void *workspace, size_t workspace_bytes, const pv_v3_diag *diag, pv_stream_t stream);
 
+/* ransac_voting_layer_v5 (RV:769-864): v3 (use v5's defaults in prm: inlier_thresh 0.999, max_iter 20,
+ * min_num 5, max_num 100) plus conf f32 [b,vn] = inlier ratio of each refined keypoint at conf_thresh
+ * (0.999 in the reference, RV:856-858); 0 for skipped images. */
+int pv_ransac_voting_v5(const pv_image_desc *img, const pv_vote_params *prm, float conf_thresh, float *out,
+                        float *conf, void *workspace, size_t workspace_bytes, const pv_v3_diag *diag,
+                        pv_stream_t stream);
+
 /* estimate_voting_distribution_with_mean (RV:333-406): mean f32 [b,vn,2] (device, input),
  * cov out f32 [b,vn,2,2].  (The reference returns `mean` unchanged.) */
 int pv_estimate_voting_distribution_with_mean(const pv_image_desc *img, const pv_vote_params *prm,

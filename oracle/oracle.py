@@ -284,6 +284,29 @@ def ransac_voting_layer_v3(mask, vertex, round_hyp_num, inlier_thresh=0.99, conf
     return out
 
 
+def ransac_voting_layer_v5(mask, vertex, round_hyp_num, inlier_thresh=0.999, confidence=0.99, max_iter=20,
+                           min_num=5, max_num=100, idxs=None, keep=None, seed=0, diag=None, conf_thresh=0.999):
+    """RV:769-864: v3's hypotheses, vote and refinement with v5's defaults,
+    plus each refined keypoint's confidence -- its inlier ratio at 0.999
+    (RV:856-858).  Returns (points [b,vn,2], confidence [b,vn])."""
+    dg = []
+    pts = ransac_voting_layer_v3(mask, vertex, round_hyp_num, inlier_thresh, confidence, max_iter, min_num,
+                                 max_num, idxs, keep, seed, dg)
+    b, vn = pts.shape[:2]
+    conf = np.zeros((b, vn), F32)
+    for bi, d in enumerate(dg):
+        if d.get("skipped"):                                    # RV:785-791
+            continue
+        tn = d["tn"]
+        inl = np.zeros((1, vn, tn), np.uint8)
+        voting_for_hypothesis(d["direct"], d["coords"], pts[bi][None], inl, conf_thresh)
+        d["conf_counts"] = inl.sum(2)[0]
+        conf[bi] = inl.sum(2)[0].astype(F32) / F32(tn)
+    if diag is not None:
+        diag.extend(dg)
+    return pts, conf
+
+
 def _evd_collect(mask, vertex, round_hyp_num, min_hyp_num, inlier_thresh, min_num, max_num,
                  idxs, keep, seed, guard_hyp_num):
     mask, vertex = np.asarray(mask), np.asarray(vertex, dtype=F32)

@@ -169,6 +169,7 @@ struct Workspace {
     int32_t *ticket;    // [b][1 + vn]   zeroed by k_fg_count: per image, per (image, keypoint)
     uint32_t *exotic;   // [b][nchv]     zeroed by k_fg_count (chunk holds a pixel outside the fast domain)
     int32_t *dsagg;     // [b][nblk]     zeroed by k_fg_count: downsampled count + 1 per block (look-back)
+    int32_t *confc;     // [b][vn][2]    zeroed by k_fg_count: v5 confidence count, ticket
     int64_t nchv;       // vote chunks per image (capacity)
     int64_t zero_words; // counts + ticket + exotic + dsagg (contiguous)
     int32_t *tn;        // [b] compacted pixels (0 = image skipped)
@@ -192,11 +193,12 @@ Workspace carve(void *base, int b, int H, int W, int vn, int nh) {
     int64_t off = 0;
     auto take = [&](int64_t bytes) { char *q = p ? p + off : nullptr; off = align_up(off + bytes, 256); return q; };
     w.nchv = (P + kVoteChunk - 1) / kVoteChunk;
-    w.zero_words = (int64_t)b * vn * nh + (int64_t)b * (1 + vn) + b * w.nchv + b * nblk;
+    w.zero_words = (int64_t)b * vn * nh + (int64_t)b * (1 + vn) + b * w.nchv + b * nblk + 2 * (int64_t)b * vn;
     w.counts = (int32_t *)take(4 * w.zero_words);
     w.ticket = w.counts ? w.counts + (int64_t)b * vn * nh : nullptr;
     w.exotic = w.counts ? (uint32_t *)(w.ticket + (int64_t)b * (1 + vn)) : nullptr;
     w.dsagg = w.counts ? (int32_t *)(w.exotic + b * w.nchv) : nullptr;
+    w.confc = w.counts ? w.dsagg + b * nblk : nullptr;
     w.tn = (int32_t *)take(4 * b);
     w.fgtot = (int32_t *)take(4 * b);
     w.blkcnt = (int32_t *)take(4 * b * nblk);
@@ -1061,6 +1063,35 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
 }
 
 // ==========================================================================
+// v5 confidence (RV:856-858): the inlier ratio of each refined keypoint at
+// a second threshold (0.999), counted over the image's compacted pixels.
+// ==========================================================================
+__global__ __launch_bounds__(256) void k_point_conf(const float *pts, const float4 *pex, const int32_t *tn, int64_t P,
+                                                    int vn, float thr, int32_t *confc, float *conf) {
+    const int j = blockIdx.x, v = blockIdx.y, b = blockIdx.z;
+    const int n = tn[b];
+    __shared__ int sh[8];
+    const float px = pts[((int64_t)b * vn + v) * 2], py = pts[((int64_t)b * vn + v) * 2 + 1];
+    const float4 *eb = pex + ((int64_t)b * vn + v) * P;
+    int c = 0;
+    for (int t = j * 256 + threadIdx.x; t < n; t += kRefineNJ * 256) {
+        const float4 e = eb[t];   // (cx, cy, nx, ny)
+        c += exact_vote(e.z, e.w, e.x, e.y, px, py, thr) ? 1 : 0;
+    }
+    c = block_sum2(c, 0, sh).x;
+    if (threadIdx.x == 0) {
+        int32_t *cc = confc + ((int64_t)b * vn + v) * 2;
+        if (c) atomicAdd(&cc[0], c);
+        __threadfence();
+        const int t = __hip_atomic_fetch_add(&cc[1], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == kRefineNJ - 1) {
+            const int total = ld_agent(&cc[0]);
+            conf[(int64_t)b * vn + v] = n > 0 ? (float)total / (float)n : 0.f;   // RV:858 float division
+        }
+    }
+}
+
+// ==========================================================================
 // EVD (RV:333-406, RV:263-331): per (image, keypoint) over all hypotheses.
 // ==========================================================================
 __global__ __launch_bounds__(256) void k_evd_with_mean(const int32_t *counts, const float2 *hyp, const int32_t *fg,
@@ -1912,6 +1943,19 @@ int pv_ransac_voting_v3(const pv_image_desc *img, const pv_vote_params *prm, flo
         if (e != hipSuccess) return rc(e);
     }
     return PV_OK;
+}
+
+int pv_ransac_voting_v5(const pv_image_desc *img, const pv_vote_params *prm, float conf_thresh, float *out,
+                        float *conf, void *workspace, size_t workspace_bytes, const pv_v3_diag *diag,
+                        pv_stream_t stream) {
+    if (!conf) return PV_EINVAL;
+    int r = pv_ransac_voting_v3(img, prm, out, workspace, workspace_bytes, diag, stream);
+    if (r) return r;
+    Workspace w = carve(workspace, img->b, img->H, img->W, img->vn, prm->round_hyp_num);
+    const int64_t P = (int64_t)img->H * img->W;
+    k_point_conf<<<dim3(kRefineNJ, img->vn, img->b), 256, 0, (hipStream_t)stream>>>(out, w.pex, w.tn, P, img->vn,
+                                                                                     conf_thresh, w.confc, conf);
+    return last();
 }
 
 static int evd_front(const pv_image_desc *img, const pv_vote_params *prm, void *workspace, size_t workspace_bytes,

@@ -35,7 +35,8 @@ import torch
 
 from . import _lib
 
-__all__ = ["ransac_voting_layer_v3", "estimate_voting_distribution_with_mean", "estimate_voting_distribution",
+__all__ = ["ransac_voting_layer_v3", "ransac_voting_layer_v5", "estimate_voting_distribution_with_mean",
+           "estimate_voting_distribution",
            "b_inv", "ransac_voting_layer_v3_from_network", "VotingWorkspace"]
 
 _MASK_KIND = {torch.int64: _lib.PV_MASK_I64, torch.uint8: _lib.PV_MASK_U8, torch.bool: _lib.PV_MASK_U8,
@@ -133,7 +134,7 @@ def _aux(x, dtype, device, shape, name):
 
 
 def _v3(d, mask, vertex, round_hyp_num, inlier_thresh, confidence, max_iter, min_num, max_num, _idxs, _keep, _diag,
-        _seed, _workspace, out=None):
+        _seed, _workspace, out=None, conf_thresh=None):
     dev = vertex.device
     b, h, w, vn = d.b, d.H, d.W, d.vn
     idxs = _aux(_idxs, torch.int32, dev, (b, round_hyp_num, vn, 2), "_idxs")
@@ -156,16 +157,24 @@ def _v3(d, mask, vertex, round_hyp_num, inlier_thresh, confidence, max_iter, min
                   ata=torch.empty((b, vn, 2, 2), dtype=torch.float32, device=dev),
                   atb=torch.empty((b, vn, 2), dtype=torch.float32, device=dev))
         diag = _lib.V3Diag(**{k: v.data_ptr() for k, v in dt.items()})
+    conf = None
     with torch.cuda.device(dev):
-        code = L.pv_ransac_voting_v3(ctypes.byref(d), ctypes.byref(prm), out.data_ptr(), ws.data_ptr(), nbytes,
-                                     ctypes.byref(diag) if diag is not None else None,
-                                     torch.cuda.current_stream(dev).cuda_stream)
-    _lib.check(code, "ransac_voting_layer_v3")
+        if conf_thresh is None:
+            code = L.pv_ransac_voting_v3(ctypes.byref(d), ctypes.byref(prm), out.data_ptr(), ws.data_ptr(), nbytes,
+                                         ctypes.byref(diag) if diag is not None else None,
+                                         torch.cuda.current_stream(dev).cuda_stream)
+        else:
+            conf = torch.empty((b, vn), dtype=torch.float32, device=dev)
+            code = L.pv_ransac_voting_v5(ctypes.byref(d), ctypes.byref(prm), float(conf_thresh), out.data_ptr(),
+                                         conf.data_ptr(), ws.data_ptr(), nbytes,
+                                         ctypes.byref(diag) if diag is not None else None,
+                                         torch.cuda.current_stream(dev).cuda_stream)
+    _lib.check(code, "ransac_voting_layer_v3" if conf_thresh is None else "ransac_voting_layer_v5")
     if _diag is not None:
         _diag.update(dt)
     # keep the inputs alive until the kernels that read them have been queued
     del mask, idxs, keep
-    return out
+    return out if conf is None else (out, conf)
 
 
 def ransac_voting_layer_v3(mask, vertex, round_hyp_num, inlier_thresh=0.99, confidence=0.99, max_iter=100,
@@ -181,6 +190,17 @@ def ransac_voting_layer_v3(mask, vertex, round_hyp_num, inlier_thresh=0.99, conf
     d = _desc(mask, vertex)
     return _v3(d, mask, vertex, round_hyp_num, inlier_thresh, confidence, max_iter, min_num, max_num, _idxs,
                _keep, _diag, _seed, _workspace)
+
+
+def ransac_voting_layer_v5(mask, vertex, round_hyp_num, inlier_thresh=0.999, confidence=0.99, max_iter=20,
+                           min_num=5, max_num=100, *, _idxs=None, _keep=None, _diag=None, _seed=None,
+                           _workspace=None):
+    """RV:769-864 (the uncertainty eval wrapper's layer, TRAIN:123): v3 with
+    v5's defaults, returning (points f32 [b,vn,2], confidence f32 [b,vn]) --
+    each refined keypoint's inlier ratio at 0.999 (RV:856-858)."""
+    d = _desc(mask, vertex)
+    return _v3(d, mask, vertex, round_hyp_num, inlier_thresh, confidence, max_iter, min_num, max_num, _idxs,
+               _keep, _diag, _seed, _workspace, conf_thresh=0.999)
 
 
 def ransac_voting_layer_v3_from_network(seg_pred, vertex_pred, round_hyp_num, inlier_thresh=0.99, confidence=0.99,

@@ -291,6 +291,7 @@ def main():
 
     # ---- G3: edge cases on small frames -----------------------------------
     edge_cases(RV, stub)
+    v5_cases(RV, stub, m64, vertex, cat_in)
     vp_kernels(stub)
 
 
@@ -391,6 +392,62 @@ def edge_cases(RV, stub):
     save("edge_cases", **out)
 
 
+def v5_records(stub):
+    """Per image of ransac_voting_layer_v5 (RV:769-864): the first gen+vote,
+    then the refine vote (hn=1) and the confidence vote (hn=1, thr 0.999)."""
+    idxs, hyps, counts, refc, confc, coords = [], [], [], [], [], []
+    calls, i = stub.calls, 0
+    while i < len(calls):
+        c = calls[i]
+        if c["kind"] == "gen":
+            idxs.append(c["idxs"]); hyps.append(c["hyp"]); coords.append(c["coords"])
+            counts.append(calls[i + 1]["counts"])
+            j = i + 2
+            while j < len(calls) and calls[j]["kind"] == "gen":
+                j += 2
+            refc.append(calls[j]["counts"][0])
+            confc.append(calls[j + 1]["counts"][0])
+            i = j + 2
+        else:
+            i += 1
+    return idxs, hyps, counts, refc, confc, coords
+
+
+def v5_cases(RV, stub, cat_m64, cat_vertex, cat_in):
+    """ransac_voting_layer_v5 as the uncertainty eval wrapper calls it
+    (TRAIN:123: hn=128, inlier_thresh=0.99, max_num=100; confidence vote at
+    0.999): the cat field, and a batch of two small fields (downsampled /
+    fewer than min_num=5 foreground pixels)."""
+    out = {}
+    torch.manual_seed(31)
+    stub.calls.clear()
+    kp, conf = RV.ransac_voting_layer_v5(torch.from_numpy(cat_m64), torch.from_numpy(cat_vertex), 128,
+                                         inlier_thresh=0.99, max_num=100)
+    idxs, hyps, counts, refc, confc, coords = v5_records(stub)
+    keep = np.zeros((480, 640), bool)
+    keep[coords[0][:, 1].astype(int), coords[0][:, 0].astype(int)] = True
+    out.update(cat_keypoints=kp.numpy(), cat_conf=conf.numpy(), cat_idxs=np.stack(idxs), cat_hyp=np.stack(hyps),
+               cat_counts=np.stack(counts), cat_refine_counts=np.stack(refc), cat_conf_counts=np.stack(confc),
+               cat_keep_bits=np.packbits(keep)[None], **cat_in)
+    H, W = 40, 48
+    fa, va = small_field(41)
+    fb, vb = small_field(42, radius=1.0)                  # 5 px: min_num is 5 -> still voted? (< 5 skips)
+    masks = np.stack([fa["mask"].astype(np.int64), np.zeros((H, W), np.int64)])
+    masks[1, 20, 24] = 1                                  # 1 foreground pixel < min_num=5 -> zeros
+    verts = np.stack([va, vb])
+    torch.manual_seed(32)
+    stub.calls.clear()
+    kp, conf = RV.ransac_voting_layer_v5(torch.from_numpy(masks), torch.from_numpy(verts), 32,
+                                         inlier_thresh=0.99, max_num=100)
+    idxs, hyps, counts, refc, confc, coords = v5_records(stub)
+    keep = np.zeros((2, H, W), bool)
+    keep[0, coords[0][:, 1].astype(int), coords[0][:, 0].astype(int)] = True
+    out.update(s_mask=masks, s_vertex=verts, s_keypoints=kp.numpy(), s_conf=conf.numpy(), s_idxs=np.stack(idxs),
+               s_hyp=np.stack(hyps), s_counts=np.stack(counts), s_refine_counts=np.stack(refc),
+               s_conf_counts=np.stack(confc), s_keep=keep)
+    save("v5_cases", **out)
+
+
 def vp_kernels(stub):
     rng = np.random.default_rng(21)
     tn, vn, hn = 300, 4, 40
@@ -404,5 +461,20 @@ def vp_kernels(stub):
     save("vp_kernels", direct=direct, coords=coords, idxs=idxs, hyp=hyp.numpy(), inliers=inl.numpy())
 
 
+def main_v5():
+    """Only the v5 fixtures (python tests/golden/make_golden.py v5)."""
+    install_shims()
+    stub = TorchKernels()
+    RV = load_reference(stub)
+    mask, pts3d, pose, p2d = demo_cat()
+    field = synth.gt_vertex_field(mask, p2d)
+    vnet = synth.to_network_layout(field)
+    vertex = torch.from_numpy(vnet).permute(0, 2, 3, 1).reshape(1, 480, 640, 9, 2).numpy()
+    m64 = mask.astype(np.int64)[None]
+    cat_in = dict(mask_bits=np.packbits(mask.astype(bool)), points_2d=p2d, pose=pose, points_3d=pts3d,
+                  field_sha=sha(field))
+    v5_cases(RV, stub, m64, vertex, cat_in)
+
+
 if __name__ == "__main__":
-    main()
+    main_v5() if sys.argv[1:] == ["v5"] else main()

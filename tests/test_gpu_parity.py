@@ -331,3 +331,28 @@ def test_fractional_coordinates_and_ragged_rows(device, rv):
         np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"tn={tn}")
         cnt = rv.vote_counts(cu(direct, device), cu(coords, device), cu(hyp, device), 0.99).cpu().numpy()
         np.testing.assert_array_equal(cnt, ref.sum(2), err_msg=f"tn={tn}")
+
+
+def test_v5_confidence_matches_reference(device, rvg):
+    """ransac_voting_layer_v5 as TRAIN:123 calls it (hn=128, 0.99, max_num=100):
+    hypotheses and counts bit-exact, keypoints within tolerance, and the 0.999
+    confidence equal to the reference's."""
+    g = G.load("v5_cases")
+    mask, vertex, _ = G.cat_inputs(g)
+    keep = np.unpackbits(g["cat_keep_bits"][0])[: 480 * 640].reshape(1, 480, 640)
+    diag = {}
+    kp, conf = rvg.ransac_voting_layer_v5(cu(mask, device), cu(vertex, device), 128, inlier_thresh=0.99,
+                                          max_num=100, _idxs=g["cat_idxs"], _keep=keep, _diag=diag)
+    np.testing.assert_array_equal(diag["counts"].cpu().numpy()[0].T, g["cat_counts"][0])
+    np.testing.assert_allclose(kp.cpu().numpy(), g["cat_keypoints"], atol=KP_TOL, rtol=0)
+    np.testing.assert_array_equal(conf.cpu().numpy(), g["cat_conf"])
+    # batch: a downsampled small field and one below min_num (zeros)
+    idxs = np.zeros((2,) + g["s_idxs"].shape[1:], np.int32)
+    idxs[0] = g["s_idxs"][0]
+    diag = {}
+    kp, conf = rvg.ransac_voting_layer_v5(cu(g["s_mask"], device), cu(g["s_vertex"], device), 32,
+                                          inlier_thresh=0.99, max_num=100, _idxs=idxs,
+                                          _keep=g["s_keep"].astype(np.uint8), _diag=diag)
+    np.testing.assert_array_equal(diag["counts"].cpu().numpy()[0].T, g["s_counts"][0])
+    np.testing.assert_allclose(kp.cpu().numpy(), g["s_keypoints"], atol=KP_TOL, rtol=0)
+    np.testing.assert_array_equal(conf.cpu().numpy(), g["s_conf"])

@@ -140,3 +140,25 @@ def test_b_inv_semantics():
     np.testing.assert_allclose(O.b_inv(A), np.linalg.inv(A), rtol=1e-6)
     A[1] = 0                                          # one singular -> identity for all (RV:514-517)
     np.testing.assert_array_equal(O.b_inv(A), np.broadcast_to(np.eye(2, dtype=np.float32), A.shape))
+
+
+def test_v5_matches_reference_golden():
+    """ransac_voting_layer_v5 (RV:769-864, called as TRAIN:123): keypoints and
+    the 0.999 confidence, with the reference's idxs and downsampling keep-mask."""
+    g = G.load("v5_cases")
+    mask, vertex = G.cat_inputs(g)[:2]
+    keep = np.unpackbits(g["cat_keep_bits"])[: 480 * 640].reshape(1, 480, 640).astype(bool)
+    dg = []
+    kp, conf = O.ransac_voting_layer_v5(mask, vertex, 128, inlier_thresh=0.99, max_num=100, idxs=g["cat_idxs"],
+                                        keep=keep, diag=dg)
+    np.testing.assert_array_equal(dg[0]["counts"], g["cat_counts"][0])
+    np.testing.assert_array_equal(dg[0]["conf_counts"], g["cat_conf_counts"][0])
+    np.testing.assert_allclose(kp, g["cat_keypoints"], atol=KP_TOL)
+    np.testing.assert_array_equal(conf, g["cat_conf"])
+    dg = []
+    kp, conf = O.ransac_voting_layer_v5(g["s_mask"], g["s_vertex"], 32, inlier_thresh=0.99, max_num=100,
+                                        idxs=[g["s_idxs"][0], None], keep=g["s_keep"], diag=dg)
+    np.testing.assert_array_equal(dg[0]["counts"], g["s_counts"][0])
+    np.testing.assert_array_equal(dg[0]["conf_counts"], g["s_conf_counts"][0])
+    np.testing.assert_allclose(kp, g["s_keypoints"], atol=KP_TOL)
+    np.testing.assert_array_equal(conf, g["s_conf"])
