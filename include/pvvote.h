@@ -138,6 +138,10 @@ int pv_ransac_voting_v5(const pv_image_desc *img, const pv_vote_params *prm, flo
                         float *conf, void *workspace, size_t workspace_bytes, const pv_v3_diag *diag,
                         pv_stream_t stream);
 
+/* ransac_motion_voting (RV:966-987): out f32 [b,vn,2] = mean over the foreground (mask.byte() != 0) of
+ * vertex + (col, row); zeros for an empty foreground.  mask kinds I64/U8/I32. */
+int pv_ransac_motion_voting(const pv_image_desc *img, float *out, pv_stream_t stream);
+
 /* estimate_voting_distribution_with_mean (RV:333-406): mean f32 [b,vn,2] (device, input),
  * cov out f32 [b,vn,2,2].  (The reference returns `mean` unchanged.) */
 int pv_estimate_voting_distribution_with_mean(const pv_image_desc *img, const pv_vote_params *prm,

@@ -307,6 +307,23 @@ def ransac_voting_layer_v5(mask, vertex, round_hyp_num, inlier_thresh=0.999, con
     return pts, conf
 
 
+def ransac_motion_voting(mask, vertex):
+    """RV:966-987: per image and keypoint the mean over the foreground
+    (mask.byte() != 0) of vertex + (col, row); zeros for an empty mask.
+    fp32 per-element add as the reference, fp64 mean."""
+    mask, vertex = np.asarray(mask), np.asarray(vertex, dtype=F32)
+    b, h, w, vn, _ = vertex.shape
+    out = np.zeros((b, vn, 2), F32)
+    for bi in range(b):
+        fg = fg_mask_v3(mask[bi])
+        if not fg.any():
+            continue
+        rows, cols = np.nonzero(fg)
+        c = np.stack([cols, rows], 1).astype(F32)[:, None, :]          # [tn,1,2] (x=col, y=row)
+        out[bi] = (vertex[bi][rows, cols] + c).astype(np.float64).mean(0).astype(F32)
+    return out
+
+
 def _evd_collect(mask, vertex, round_hyp_num, min_hyp_num, inlier_thresh, min_num, max_num,
                  idxs, keep, seed, guard_hyp_num):
     mask, vertex = np.asarray(mask), np.asarray(vertex, dtype=F32)

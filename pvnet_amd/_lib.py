@@ -54,6 +54,7 @@ SIGNATURES = [
     ("pv_ransac_voting_v5", ctypes.c_int,
      [ctypes.POINTER(ImageDesc), ctypes.POINTER(VoteParams), c_f32, c_vp, c_vp, c_vp, c_size, ctypes.POINTER(V3Diag),
       c_vp]),
+    ("pv_ransac_motion_voting", ctypes.c_int, [ctypes.POINTER(ImageDesc), c_vp, c_vp]),
     ("pv_estimate_voting_distribution_with_mean", ctypes.c_int,
      [ctypes.POINTER(ImageDesc), ctypes.POINTER(VoteParams), c_vp, c_vp, c_vp, c_size, c_vp]),
     ("pv_estimate_voting_distribution", ctypes.c_int,

@@ -1063,6 +1063,70 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
 }
 
 // ==========================================================================
+// ransac_motion_voting (RV:966-987): per image and keypoint, the mean over
+// the foreground (mask.byte() != 0) of vertex + (col, row) -- the vertex
+// field holds offsets here.  fp64 sums (torch.mean's fp32 order is
+// unspecified), block-local in LDS, then one device-scope add per block; the
+// last block of each image divides.  Empty foreground -> zeros (RV:977-979).
+// ==========================================================================
+template <int KIND>
+__global__ __launch_bounds__(256) void k_motion_vote(MaskView m, VertexView vx, int H, int W, int vn, double *acc,
+                                                     int32_t *cnt, int32_t *ticket, float *out) {
+    const int b = blockIdx.y, nblk = gridDim.x;
+    __shared__ double sacc[64 * 2];
+    __shared__ int scnt;
+    for (int i = threadIdx.x; i < vn * 2; i += 256) sacc[i] = 0.0;
+    if (threadIdx.x == 0) scnt = 0;
+    __syncthreads();
+    const uint32_t p = (uint32_t)blockIdx.x * 256 + threadIdx.x;
+    if (p < (uint32_t)H * W) {
+        const int r = (int)(p / (uint32_t)W), c = (int)(p - (uint32_t)r * W);
+        if (is_fg<KIND, false>(m, b, r, c)) {
+            atomicAdd(&scnt, 1);
+            const int64_t vo = b * vx.s[0] + r * vx.s[1] + c * vx.s[2];
+            for (int v = 0; v < vn; ++v) {
+                float dx, dy;
+                if (vx.kind == PV_VERTEX_F32) {
+                    dx = ((const float *)vx.p)[vo + v * vx.s[3]];
+                    dy = ((const float *)vx.p)[vo + v * vx.s[3] + vx.s[4]];
+                } else {
+                    dx = __half2float(((const __half *)vx.p)[vo + v * vx.s[3]]);
+                    dy = __half2float(((const __half *)vx.p)[vo + v * vx.s[3] + vx.s[4]]);
+                }
+                atomicAdd(&sacc[v * 2], (double)(dx + (float)c));       // RV:983 vertex + coords (fp32 add)
+                atomicAdd(&sacc[v * 2 + 1], (double)(dy + (float)r));
+            }
+        }
+    }
+    __syncthreads();
+    if (scnt) {
+        for (int i = threadIdx.x; i < vn * 2; i += 256) atomicAdd(&acc[(int64_t)b * vn * 2 + i], sacc[i]);
+        if (threadIdx.x == 0) atomicAdd(&cnt[b], scnt);
+    }
+    __syncthreads();
+    __shared__ int slast;
+    if (threadIdx.x == 0) {
+        __threadfence();
+        slast = __hip_atomic_fetch_add(&ticket[b], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1;
+    }
+    __syncthreads();
+    if (!slast) return;
+    const int n = ld_agent(&cnt[b]);
+    for (int i = threadIdx.x; i < vn * 2; i += 256)
+        out[(int64_t)b * vn * 2 + i] = n > 0 ? (float)(ld_agent(&acc[(int64_t)b * vn * 2 + i]) / n) : 0.f;
+}
+
+template <int KIND, bool EVD>
+struct MotionStage {
+    static int run(const MaskView *m, const VertexView *vx, int b, int H, int W, int vn, double *acc, int32_t *cnt,
+                   int32_t *ticket, float *out, hipStream_t s) {
+        dim3 grid((unsigned)(((int64_t)H * W + 255) / 256), (unsigned)b);
+        k_motion_vote<KIND><<<grid, 256, 0, s>>>(*m, *vx, H, W, vn, acc, cnt, ticket, out);
+        return PV_OK;
+    }
+};
+
+// ==========================================================================
 // v5 confidence (RV:856-858): the inlier ratio of each refined keypoint at
 // a second threshold (0.999), counted over the image's compacted pixels.
 // ==========================================================================
@@ -1956,6 +2020,33 @@ int pv_ransac_voting_v5(const pv_image_desc *img, const pv_vote_params *prm, flo
     k_point_conf<<<dim3(kRefineNJ, img->vn, img->b), 256, 0, (hipStream_t)stream>>>(out, w.pex, w.tn, P, img->vn,
                                                                                      conf_thresh, w.confc, conf);
     return last();
+}
+
+int pv_ransac_motion_voting(const pv_image_desc *img, float *out, pv_stream_t stream) {
+    int r = check_desc(img);
+    if (r) return r;
+    if (!out || img->mask_kind == PV_MASK_SEG_F32 || img->mask_kind == PV_MASK_SEG_F16) return PV_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const int b = img->b, vn = img->vn;
+    // stream-ordered, zeroed scratch: sums [b][vn][2] f64, counts [b], tickets [b]
+    const size_t acc_bytes = sizeof(double) * 2 * (size_t)b * vn, bytes = acc_bytes + sizeof(int32_t) * 2 * b;
+    char *scr = nullptr;
+    hipError_t e = hipMallocAsync((void **)&scr, bytes, s);
+    if (e != hipSuccess) return rc(e);
+    e = hipMemsetAsync(scr, 0, bytes, s);
+    if (e != hipSuccess) return rc(e);
+    MaskView m{img->mask, img->mask_strides[0], img->mask_strides[1], img->mask_strides[2], img->mask_strides[3]};
+    VertexView vx;
+    vx.p = img->vertex;
+    vx.kind = img->vertex_kind;
+    for (int i = 0; i < 5; ++i) vx.s[i] = img->vertex_strides[i];
+    int32_t *cnt = (int32_t *)(scr + acc_bytes);
+    r = dispatch_mask<MotionStage>(img->mask_kind, false, (const MaskView *)&m, (const VertexView *)&vx, b, img->H,
+                                   img->W, vn, (double *)scr, cnt, cnt + b, out, s);
+    if (r) return r;
+    r = last();
+    e = hipFreeAsync(scr, s);
+    return r ? r : rc(e);
 }
 
 static int evd_front(const pv_image_desc *img, const pv_vote_params *prm, void *workspace, size_t workspace_bytes,

@@ -35,7 +35,8 @@ import torch
 
 from . import _lib
 
-__all__ = ["ransac_voting_layer_v3", "ransac_voting_layer_v5", "estimate_voting_distribution_with_mean",
+__all__ = ["ransac_voting_layer_v3", "ransac_voting_layer_v5", "ransac_motion_voting",
+           "estimate_voting_distribution_with_mean",
            "estimate_voting_distribution",
            "b_inv", "ransac_voting_layer_v3_from_network", "VotingWorkspace"]
 
@@ -201,6 +202,19 @@ def ransac_voting_layer_v5(mask, vertex, round_hyp_num, inlier_thresh=0.999, con
     d = _desc(mask, vertex)
     return _v3(d, mask, vertex, round_hyp_num, inlier_thresh, confidence, max_iter, min_num, max_num, _idxs,
                _keep, _diag, _seed, _workspace, conf_thresh=0.999)
+
+
+def ransac_motion_voting(mask, vertex):
+    """RV:966-987: mask [b,h,w], vertex [b,h,w,vn,2] holding offsets ->
+    f32 [b,vn,2], the foreground mean of vertex + (col, row) (zeros for an
+    empty mask), in one HIP kernel."""
+    d = _desc(mask, vertex)
+    out = torch.empty((d.b, d.vn, 2), dtype=torch.float32, device=vertex.device)
+    with torch.cuda.device(vertex.device):
+        code = _lib.load().pv_ransac_motion_voting(ctypes.byref(d), out.data_ptr(),
+                                                   torch.cuda.current_stream(vertex.device).cuda_stream)
+    _lib.check(code, "ransac_motion_voting")
+    return out
 
 
 def ransac_voting_layer_v3_from_network(seg_pred, vertex_pred, round_hyp_num, inlier_thresh=0.99, confidence=0.99,

@@ -292,6 +292,7 @@ def main():
     # ---- G3: edge cases on small frames -----------------------------------
     edge_cases(RV, stub)
     v5_cases(RV, stub, m64, vertex, cat_in)
+    motion_cases(RV)
     vp_kernels(stub)
 
 
@@ -448,6 +449,24 @@ def v5_cases(RV, stub, cat_m64, cat_vertex, cat_in):
     save("v5_cases", **out)
 
 
+def motion_cases(RV):
+    """ransac_motion_voting (RV:966-987) on offset fields: a 480x640 disk
+    (29,861 px), a small field, an empty mask."""
+    out = {}
+    rng = np.random.default_rng(51)
+    H, W, vn = 120, 160, 4
+    masks = np.zeros((3, H, W), np.int64)
+    yy, xx = np.mgrid[0:H, 0:W]
+    masks[0] = ((xx - 80) ** 2 + (yy - 60) ** 2 <= 40 ** 2)
+    masks[1] = ((xx - 30) ** 2 + (yy - 100) ** 2 <= 9 ** 2) * 2          # byte() of 2 -> foreground
+    kp = rng.uniform([20, 20], [140, 100], (3, vn, 2)).astype(np.float32)
+    off = kp[:, None, None] - np.stack([xx, yy], -1)[None, :, :, None].astype(np.float32)
+    verts = (off + rng.normal(0, 2.0, off.shape)).astype(np.float32) * (masks != 0)[..., None, None]
+    pts = RV.ransac_motion_voting(torch.from_numpy(masks), torch.from_numpy(verts)).numpy()
+    out.update(mask=masks, vertex=verts, points=pts)
+    save("motion_cases", **out)
+
+
 def vp_kernels(stub):
     rng = np.random.default_rng(21)
     tn, vn, hn = 300, 4, 40
@@ -476,5 +495,11 @@ def main_v5():
     v5_cases(RV, stub, m64, vertex, cat_in)
 
 
+def main_motion():
+    install_shims()
+    RV = load_reference(TorchKernels())
+    motion_cases(RV)
+
+
 if __name__ == "__main__":
-    main_v5() if sys.argv[1:] == ["v5"] else main()
+    {"v5": main_v5, "motion": main_motion}.get(sys.argv[1] if sys.argv[1:] else "", main)()

@@ -356,3 +356,13 @@ def test_v5_confidence_matches_reference(device, rvg):
     np.testing.assert_array_equal(diag["counts"].cpu().numpy()[0].T, g["s_counts"][0])
     np.testing.assert_allclose(kp.cpu().numpy(), g["s_keypoints"], atol=KP_TOL, rtol=0)
     np.testing.assert_array_equal(conf.cpu().numpy(), g["s_conf"])
+
+
+def test_motion_voting(device, rvg):
+    """ransac_motion_voting (RV:966-987): the reference's own outputs (fp32
+    torch.mean) within 1e-3 px, the oracle's fp64 mean within 1e-4 px."""
+    g = G.load("motion_cases")
+    got = rvg.ransac_motion_voting(cu(g["mask"], device), cu(g["vertex"], device)).cpu().numpy()
+    np.testing.assert_allclose(got, g["points"], atol=1e-3, rtol=0)
+    np.testing.assert_allclose(got, O.ransac_motion_voting(g["mask"], g["vertex"]), atol=1e-4, rtol=0)
+    assert np.all(got[2] == 0)

@@ -162,3 +162,8 @@ def test_v5_matches_reference_golden():
     np.testing.assert_array_equal(dg[0]["conf_counts"], g["s_conf_counts"][0])
     np.testing.assert_allclose(kp, g["s_keypoints"], atol=KP_TOL)
     np.testing.assert_array_equal(conf, g["s_conf"])
+
+
+def test_motion_voting_matches_reference_golden():
+    g = G.load("motion_cases")
+    np.testing.assert_allclose(O.ransac_motion_voting(g["mask"], g["vertex"]), g["points"], atol=1e-3, rtol=0)
