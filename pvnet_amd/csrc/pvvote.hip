@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -470,6 +471,7 @@ struct VoteArgs {
     uint64_t seed;
     int32_t P, raw_v, raw_t, exotic_b, cnt_v, cnt_h, cnt_bs;
     int32_t tn_host, b, vn, nh, hgn, fast;
+    int32_t b_base;             // first image of this launch (RNG keys stay per global image)
     float thr, tau, gzf, gzr;
     uint64_t *trace;            // debug: per-wave (start, end) s_memrealtime stamps, or nullptr
 };
@@ -498,8 +500,9 @@ __device__ __forceinline__ float2 item_hyp(const VoteArgs &a, int b, int v, int 
                 t0 = min(max(a.idxs[gid * 2], 0), n - 1);
                 t1 = min(max(a.idxs[gid * 2 + 1], 0), n - 1);
             } else {
-                t0 = rand_index(a.seed, (uint64_t)gid * 2, n);
-                t1 = rand_index(a.seed, (uint64_t)gid * 2 + 1, n);
+                const uint64_t key = (uint64_t)gid + (uint64_t)a.b_base * a.nh * a.vn;
+                t0 = rand_index(a.seed, key * 2, n);
+                t1 = rand_index(a.seed, key * 2 + 1, n);
             }
             const F4 e0 = pixel_exact<PREPPED>(a, b, v, t0), e1 = pixel_exact<PREPPED>(a, b, v, t1);
             float ox, oy;
@@ -514,6 +517,13 @@ __device__ __forceinline__ float2 item_hyp(const VoteArgs &a, int b, int v, int 
         x = q.x; y = q.y;
     }
     return make_float2(x, y);
+}
+
+// wave w's share [lo, hi) of `total` items cut evenly over `nwaves` (32-bit: the callers keep total < 2^31)
+__device__ __forceinline__ void even_share(uint32_t total, uint32_t nwaves, uint32_t w, uint32_t *lo, uint32_t *hi) {
+    const uint32_t q = total / nwaves, rem = total - q * nwaves;
+    *lo = w * q + min(w, rem);
+    *hi = *lo + q + (w < rem ? 1u : 0u);
 }
 
 __device__ __forceinline__ float bcast(float x, int lane) {
@@ -847,25 +857,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     __shared__ ExactSlab<PREPPED> stagex_all[4];
     F4 *stage = stage_all[threadIdx.x / 64];
     ExactSlab<PREPPED> &stagex = stagex_all[threadIdx.x / 64];
-    int64_t total = 0;
-    for (int b = 0; b < a.b; ++b) total += (int64_t)a.vn * a.hgn * (a.tn_dev ? a.tn_dev[b] : a.tn_host);
-    int64_t lo = total * wave / nwaves, hi = total * (wave + 1) / nwaves;
+    // 32-bit index math (the host splits launches so that the work stays < 2^31)
+    uint32_t total = 0;
+    for (int b = 0; b < a.b; ++b) total += (uint32_t)(a.vn * a.hgn) * (uint32_t)(a.tn_dev ? a.tn_dev[b] : a.tn_host);
+    uint32_t lo, hi;
+    even_share(total, (uint32_t)nwaves, (uint32_t)wave, &lo, &hi);
     const int64_t wave_total = hi - lo;
     int nfix = 0, nseg = 0;   // diagnostics (trace)
     // walk the segments of [lo, hi)
     int b = 0;
-    int64_t base = 0;
+    uint32_t base = 0;
     while (lo < hi) {
-        int n = a.tn_dev ? a.tn_dev[b] : a.tn_host;
-        int64_t span = (int64_t)a.vn * a.hgn * n;
+        const int n = a.tn_dev ? a.tn_dev[b] : a.tn_host;
+        const uint32_t span = (uint32_t)(a.vn * a.hgn) * (uint32_t)n;
         if (lo >= base + span) { base += span; ++b; continue; }
-        int64_t r = lo - base;
-        int g = (int)(r / n);               // (v, hg) group index
-        int ts = (int)(r - (int64_t)g * n);
-        int te = (int)min<int64_t>((int64_t)n, ts + (hi - lo));
-        int v = g / a.hgn, hg = g % a.hgn;
+        const uint32_t r = lo - base;
+        const int g = (int)(r / (uint32_t)n);               // (v, hg) group index
+        const int ts = (int)(r - (uint32_t)g * n);
+        const int te = (int)min((uint32_t)n, ts + (hi - lo));
+        const int v = g / a.hgn, hg = g - v * a.hgn;
         vote_segment<GEN, PREPPED>(a, stage, stagex, uniform(b), uniform(v), uniform(hg), uniform(ts), uniform(te),
-                                   n, hi - lo - (te - ts), wave_total, nfix);
+                                   n, (int64_t)(hi - lo) - (te - ts), wave_total, nfix);
         lo += te - ts;
         ++nseg;
     }
@@ -1499,8 +1511,11 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, int 
         fk2[j] = ok ? -fmaf(ux, cy, -(uy * cx)) : 0.f;
     }
     // hypothesis records (lane i -> row h0 + 8i): h - o, band, exact flag
+    uint64_t flagged;                                   // rows the exact pass decides whole
     {
-        F4 rec{0.f, 0.f, 0.f, 1.f};
+        // (flagged rows carry an infinite band, so the hot loop defers them
+        // without testing the flag)
+        F4 rec{0.f, 0.f, __builtin_inff(), 1.f};
         if (lane < nh) {
             // non-finite or outside the fast domain: the exact sequence decides
             const bool xo = !(isfinite(hq.x) && isfinite(hq.y)) || hyp_exact_only(hq.x, hq.y);
@@ -1510,6 +1525,7 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, int 
                 rec = F4{hx, hy, (a.gzf + a.gzr) * B * 1.00001f, 0.f};
             }
         }
+        flagged = __builtin_amdgcn_ballot_w64(lane < nh && rec.w != 0.f);
         __builtin_amdgcn_wave_barrier();
         recs[lane] = rec;
         __builtin_amdgcn_wave_barrier();
@@ -1566,23 +1582,36 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, int 
         return m;
     };
 
-    // Hot loop: the fast decision of every pair, one 8-byte store per row
-    // (byte stores for the partial words at row ends).  Rows with a pair
-    // inside the band and rows outside the fast domain are deferred to the
-    // exact pass below, which writes them instead -- the hot loop carries no
-    // exact-sequence code.
-    uint64_t dmask = 0;                                 // deferred rows (nh <= 64)
-    F4 rec = recs[0];
-    for (int i = 0; i < nh; ++i) {
-        const F4 nrec = recs[min(i + 1, kByteHB - 1)];    // next record, one iteration ahead
-        float z[kBytePix];
-        const float m = zrow(rec, z);
-        const bool d = __builtin_amdgcn_readfirstlane(__float_as_uint(rec.w)) ||
-                       __builtin_amdgcn_ballot_w64(m <= rec.z) != 0;
-        if (d) dmask |= 1ull << i;
-        else store(orow + rstep * i, pack4(z[0], z[1], z[2], z[3]), pack4(z[4], z[5], z[6], z[7]));
-        rec = nrec;
-    }
+    // Hot loop: the fast decision of every pair, one 8-byte store per row.
+    // Rows with a pair inside the band and rows outside the fast domain are
+    // deferred to the exact pass below, which writes them instead -- the hot
+    // loop carries no exact-sequence code.  Waves holding a partial word (row
+    // ends) run the same loop with per-lane byte stores.
+    uint64_t dmask = flagged;                           // deferred rows (nh <= 64)
+    auto rows = [&](auto partial) {
+        F4 rec = recs[0];
+        uint8_t *p = orow;
+        for (int i = 0; i < nh; ++i) {
+            const F4 nrec = recs[min(i + 1, kByteHB - 1)];    // next record, one iteration ahead
+            float z[kBytePix];
+            const float m = zrow(rec, z);
+            const uint64_t hit = __builtin_amdgcn_ballot_w64(m <= rec.z);   // flagged rows: rec.z = inf
+            const uint32_t lo = pack4(z[0], z[1], z[2], z[3]), hi = pack4(z[4], z[5], z[6], z[7]);
+            if constexpr (MODE == PV_VOTE_DENSE && !decltype(partial)::value) {
+                // dense: store every row; a deferred row is rewritten by the exact pass
+                // (same lane, same address: program order)
+                *(uint2 *)p = make_uint2(lo, hi);
+                dmask |= (uint64_t)(hit != 0) << i;
+            } else {
+                if (hit) dmask |= 1ull << i;
+                else store(p, lo, hi);
+            }
+            p += rstep;
+            rec = nrec;
+        }
+    };
+    if (__builtin_amdgcn_ballot_w64(vmask != 0xffu)) rows(std::true_type{});
+    else rows(std::false_type{});
 
     // Exact pass over the deferred rows.
     while (dmask) {
@@ -1630,18 +1659,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     F4 *recs = recs_all[threadIdx.x / 64];
     const int wave = uniform((int)(blockIdx.x * 4 + threadIdx.x / 64));
     const int64_t nwaves = (int64_t)gridDim.x * 4;
-    const int64_t per_v = (int64_t)a.nwin * a.hn;          // sum over c of nwin * class_rows(c)
-    const int64_t total = per_v * a.vn;
-    int64_t lo = total * wave / nwaves, hi = total * (wave + 1) / nwaves;
+    // 32-bit index math: rows = vn * nwin * hn < 2^31 (host-checked)
+    const uint32_t per_v = (uint32_t)a.nwin * a.hn;        // sum over c of nwin * class_rows(c)
+    uint32_t lo, hi;
+    even_share(per_v * a.vn, (uint32_t)nwaves, (uint32_t)wave, &lo, &hi);
     while (lo < hi) {
         const int v = (int)(lo / per_v);
-        int64_t r = lo - (int64_t)v * per_v;
+        uint32_t r = lo - (uint32_t)v * per_v;
         int c = 0;
-        while (r >= (int64_t)a.nwin * class_rows(a.hn, c)) { r -= (int64_t)a.nwin * class_rows(a.hn, c); ++c; }
+        while (r >= (uint32_t)a.nwin * class_rows(a.hn, c)) { r -= (uint32_t)a.nwin * class_rows(a.hn, c); ++c; }
         const int nc = class_rows(a.hn, c);
-        const int w = (int)(r / nc);
-        const int i0 = (int)(r - (int64_t)w * nc);
-        const int i1 = (int)min<int64_t>((int64_t)nc, min<int64_t>(i0 + kByteHB, i0 + (hi - lo)));
+        const int w = (int)(r / (uint32_t)nc);
+        const int i0 = (int)(r - (uint32_t)w * nc);
+        const int i1 = min(nc, (int)min((uint32_t)(i0 + kByteHB), i0 + (hi - lo)));
         if (kByteWin * w - (int)((((int64_t)c * a.vn + v) * a.tn) & 7) < a.tn)   // window inside the row
             vote_bytes_seg<MODE>(a, recs, uniform(v), uniform(c), uniform(w), uniform(i0), uniform(i1));
         lo += i1 - i0;
@@ -1842,14 +1872,31 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
     va.b = b; va.vn = vn; va.nh = nh; va.hgn = (nh + kGroup - 1) / kGroup;
     fast_constants(prm->inlier_thresh, &va);
     va.trace = g_vote_trace;
-    // upper bound of the work: every pixel of every image in the foreground
-    int64_t steps_ub = (int64_t)b * vn * va.hgn * P;
     if (dg.ev_vote_begin) {
         hipError_t e = hipEventRecord((hipEvent_t)dg.ev_vote_begin, s);
         if (e != hipSuccess) return rc(e);
     }
-    k_vote_count<true, true><<<vote_grid_steps(steps_ub, (const void *)k_vote_count<true, true>), 256, 0, s>>>(va);
-    if ((r = last())) return r;
+    // the kernel indexes its work in 32 bits: images per launch such that the
+    // upper bound (every pixel of every image in the foreground) stays < 2^31
+    const int64_t per_img = (int64_t)vn * va.hgn * P;
+    const int chunk = (int)std::max<int64_t>(1, std::min<int64_t>(b, ((1ll << 31) - 1) / per_img));
+    if (per_img >= (1ll << 31)) return PV_EINVAL;
+    for (int b0 = 0; b0 < b; b0 += chunk) {
+        VoteArgs vc = va;
+        const int nb = std::min(chunk, b - b0);
+        vc.b = nb;
+        vc.b_base = b0;
+        vc.pix += (int64_t)b0 * vn * P;
+        vc.pex += (int64_t)b0 * vn * P;
+        vc.exotic += (int64_t)b0 * va.exotic_b;
+        vc.hyp_out += (int64_t)b0 * nh * vn;
+        if (vc.diag_hyp) vc.diag_hyp += (int64_t)b0 * nh * vn * 2;
+        if (vc.idxs) vc.idxs += (int64_t)b0 * nh * vn * 2;
+        vc.counts += (int64_t)b0 * va.cnt_bs;
+        vc.tn_dev += b0;
+        k_vote_count<true, true><<<vote_grid_steps(nb * per_img, (const void *)k_vote_count<true, true>), 256, 0, s>>>(vc);
+        if ((r = last())) return r;
+    }
     if (dg.ev_vote_end) return rc(hipEventRecord((hipEvent_t)dg.ev_vote_end, s));
     return PV_OK;
 }
@@ -1917,12 +1964,15 @@ int pv_voting_for_hypothesis(const float *direct, const float *coords, const flo
     const int64_t nprep = (int64_t)vn * tn + (int64_t)vn * hn;
     k_prep_api<<<(unsigned)((nprep + 255) / 256), 256, 0, s>>>(direct, coords, hypo, (float4 *)scratch,
                                                                 (float2 *)(scratch + prep_bytes), tn, vn, hn);
-    // persistent grid: every block resident, >= ~16 rows per wave
+    // persistent grid: every block resident, >= ~rpw rows per wave
     const int64_t rows = (int64_t)vn * ba.nwin * hn;
+    if (rows >= (1ll << 31)) return PV_EINVAL;   // the kernel's 32-bit row index (a >2 TB mask)
+    int64_t rpw = 16;
+    if (const char *e2 = getenv("PVVOTE_BYTES_RPW")) rpw = atoi(e2);   // experiment knob
     if (mode == PV_VOTE_DENSE)
-        k_vote_bytes<PV_VOTE_DENSE><<<vote_grid_steps(rows * 8, (const void *)k_vote_bytes<PV_VOTE_DENSE>), 256, 0, s>>>(ba);
+        k_vote_bytes<PV_VOTE_DENSE><<<vote_grid_steps(rows * 128 / rpw, (const void *)k_vote_bytes<PV_VOTE_DENSE>), 256, 0, s>>>(ba);
     else
-        k_vote_bytes<PV_VOTE_OR><<<vote_grid_steps(rows * 8, (const void *)k_vote_bytes<PV_VOTE_OR>), 256, 0, s>>>(ba);
+        k_vote_bytes<PV_VOTE_OR><<<vote_grid_steps(rows * 128 / rpw, (const void *)k_vote_bytes<PV_VOTE_OR>), 256, 0, s>>>(ba);
     int r = last();
     e = hipFreeAsync(scratch, s);
     return r ? r : rc(e);
@@ -1965,6 +2015,7 @@ int pv_vote_counts(const float *direct, const float *coords, const float *hypo, 
     va.b = 1; va.vn = vn; va.nh = hn; va.hgn = (hn + kGroup - 1) / kGroup;
     fast_constants(inlier_thresh, &va);
     if (tn == 0) return PV_OK;
+    if ((int64_t)vn * va.hgn * tn >= (1ll << 31)) return PV_EINVAL;   // the kernel's 32-bit work index
     k_vote_count<false, false><<<vote_grid_steps((int64_t)vn * va.hgn * tn, (const void *)k_vote_count<false, false>),
                                  256, 0, s>>>(va);
     return last();
