@@ -1406,6 +1406,7 @@ struct ByteArgs {
     uint8_t *out;          // [hn][vn][tn]
     int tn, vn, hn, nwin, fast;
     float thr, tau, gzf, gzr;
+    int dbg;               // profiling ablation (PVVOTE_DEBUG_BYTES), 0 = normal
 };
 
 __host__ __device__ inline int class_rows(int hn, int c) { return c < hn ? (hn - c + 7) / 8 : 0; }
@@ -1614,6 +1615,7 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, int 
     else rows(std::false_type{});
 
     // Exact pass over the deferred rows.
+    if (a.dbg == 3) dmask = 0;   // profiling ablation only
     while (dmask) {
         const int i = __builtin_ctzll(dmask);
         dmask &= dmask - 1;
@@ -1961,6 +1963,7 @@ int pv_voting_for_hypothesis(const float *direct, const float *coords, const flo
     ByteArgs ba{(const float4 *)scratch, (const float2 *)(scratch + prep_bytes), direct, coords, hypo, inliers,
                 tn, vn, hn, 0, fc.fast, fc.thr, fc.tau, fc.gzf, fc.gzr};
     ba.nwin = (tn + 7 + kByteWin - 1) / kByteWin;
+    if (const char *e3 = getenv("PVVOTE_DEBUG_BYTES")) ba.dbg = atoi(e3);
     const int64_t nprep = (int64_t)vn * tn + (int64_t)vn * hn;
     k_prep_api<<<(unsigned)((nprep + 255) / 256), 256, 0, s>>>(direct, coords, hypo, (float4 *)scratch,
                                                                 (float2 *)(scratch + prep_bytes), tn, vn, hn);

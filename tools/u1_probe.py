@@ -25,7 +25,9 @@ def timeit(fn, reps=20):
 f = synth.synthetic_field(1234)
 m = np.argmax(f["seg"][0], 0) == 1
 rows, cols = np.nonzero(m)
-VN, hn = 9, 512
+VN = 9
+import os
+hn = int(os.environ.get('U1_HN', '512'))
 for tn in (29861, 29824, 29696, 29860):
     coords = torch.from_numpy(np.stack([cols[:tn], rows[:tn]], 1).astype(np.float32)).cuda()
     direct = torch.from_numpy(np.ascontiguousarray(
