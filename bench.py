@@ -35,6 +35,17 @@ FP32_VECTOR_PEAK_TFLOPS = 157.3
 H, W, VN = 480, 640, 9
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (profiles/r01_pmc_traffic.json: 2*FETCH_SIZE + WRITE_SIZE, collected with
+    tools/pmc_traffic.sh on the same bench command), or None."""
+    try:
+        with open(os.path.join(REPO, "profiles", "r01_pmc_traffic.json")) as f:
+            return json.load(f)["kernels"][kernel]["hbm_bytes"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -246,7 +257,8 @@ def measure_u1(dev, hn=512, reps=20):
     torch.cuda.synchronize()
     ms = a.elapsed_time(b) / reps
     nbytes = 8 * tn * VN + 8 * tn + 8 * hn * VN + hn * VN * tn      # BASELINE.md U1 algorithmic bytes
-    return dict(kernel="k_vote_bytes<DENSE> (pv_voting_for_hypothesis)", bytes_per_launch=nbytes,
+    return dict(kernel="k_prep_api + k_vote_bytes<DENSE> (pv_voting_for_hypothesis)", bytes_per_launch=nbytes,
+                traffic=(pmc_traffic("k_vote_bytes") or 0) + (pmc_traffic("k_prep_api") or 0) or None,
                 ms=ms, achieved_gbs=nbytes / (ms * 1e-3) / 1e9, peak_gbs=HBM_PEAK_GBS,
                 frac=nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, hn=hn, tn=tn)
 
@@ -373,9 +385,11 @@ def report(args, ws, res, final_err, seg, ver, fb, rvg, work, dev):
     achieved = flops / (vote_ms * 1e-3) / 1e12
     roof = dict(bound="valu", kernel="k_vote_count (fused vote+count, U2)", achieved=round(achieved, 2),
                 peak=FP32_VECTOR_PEAK_TFLOPS, unit="TFLOP/s", frac=round(achieved / FP32_VECTOR_PEAK_TFLOPS, 4),
-                traffic=None, avg_kernel_ms=round(vote_ms, 5), flop_per_launch=flops,
-                note="12 FLOP per (hypothesis, keypoint, pixel) pair (SURVEY 8(d) U2); HBM traffic per launch "
-                     "~2.4 MB (no inlier mask), so the bound is the vector ALU, not HBM or MFMA")
+                traffic=pmc_traffic("k_vote_count"), avg_kernel_ms=round(vote_ms, 5), flop_per_launch=flops,
+                note="12 FLOP per (hypothesis, keypoint, pixel) pair (SURVEY 8(d) U2); compulsory bytes ~2.4 MB "
+                     "(no inlier mask), so the bound is the vector ALU, not HBM or MFMA; traffic = 2*FETCH_SIZE + "
+                     "WRITE_SIZE per launch from profiles/r01_pmc_traffic.json (the 4 hypothesis groups re-read the "
+                     "pixel operands, served largely by the Infinity Cache)")
     line = {
         "metric": "images/sec (480x640, 9 kp) vote->keypoint",
         "value": round(value, 2),

@@ -24,6 +24,8 @@ for s in "$@"; do
     prof) step prof 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$PWD/gpurun_out/prof" -o bench -- python3 bench.py --skip-cpu --skip-e2e ;;
     pmcfetch) step pmcfetch 600 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d "$PWD/gpurun_out/pmc_fetch" -o bench -- python3 bench.py --skip-cpu --skip-e2e --steps 20 ;;
     pmcwrite) step pmcwrite 600 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d "$PWD/gpurun_out/pmc_write" -o bench -- python3 bench.py --skip-cpu --skip-e2e --steps 20 ;;
+    pmchbm) step pmchbm1 600 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d "$PWD/gpurun_out/pmc_fetch" -o bench -- python3 bench.py --skip-cpu --skip-e2e --steps 20 &&
+            step pmchbm2 600 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d "$PWD/gpurun_out/pmc_write" -o bench -- python3 bench.py --skip-cpu --skip-e2e --steps 20 ;;
     pmcvalu) step pmcvalu 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -T --output-format csv -d "$PWD/gpurun_out/pmc_valu" -o bench -- python3 bench.py --skip-cpu --skip-e2e --steps 20 ;;
     listpmc) step listpmc 300 rocprofv3 -L ;;
     pmcvote) step pmcvote1 600 rocprofv3 --kernel-include-regex k_vote_count --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_INST_CYCLES_SALU -T --output-format csv -d "$PWD/gpurun_out/pmc_vote1" -o v -- python3 bench.py --skip-cpu --skip-e2e --skip-u1 --steps 10 &&
