@@ -179,6 +179,7 @@ struct Workspace {
     float4 *pex;        // [b][vn][P]   exact pixel data (cx, cy, nx, ny): reference operands
     float4 *pix;        // [b][vn][P]   fast-test data (fx, cy, ux, uy)
     float2 *hyp;        // [b][nh][vn]  (reference layout)
+    float2 *hypv;       // [b][vn][nh]  the same, keypoint-major (the vote kernel's coalesced reads)
     int32_t *win;       // [b][vn]
     float *ratio;       // [b][vn]
     double *refpart;    // [b][vn][kRefineNJ][5]
@@ -206,6 +207,7 @@ Workspace carve(void *base, int b, int H, int W, int vn, int nh) {
     w.pex = (float4 *)take(16 * b * vn * P);
     w.pix = (float4 *)take(16 * b * vn * P);
     w.hyp = (float2 *)take(8 * (int64_t)b * nh * vn);
+    w.hypv = (float2 *)take(8 * (int64_t)b * nh * vn);
     w.win = (int32_t *)take(4 * b * vn);
     w.ratio = (float *)take(4 * b * vn);
     w.refpart = (double *)take(8 * 5 * (int64_t)b * vn * kRefineNJ);
@@ -462,8 +464,10 @@ struct VoteArgs {
     const uint32_t *exotic;     // PREPPED: 256-pixel chunk holds a pixel outside the fast domain
     const float2 *coords;       // !PREPPED: coords[b*P + t]
     const float2 *raw;          // !PREPPED: raw[b*vn*P + v*raw_v + t*raw_t]
-    const float2 *hyp;          // !GEN: hyp[(b*nh + h)*vn + v]
-    float2 *hyp_out;            // GEN: generated hypotheses, same layout
+    const float2 *hyp;          // !GEN: hyp[b*hyp_sb + v*hyp_sv + h*hyp_sh]
+    float2 *hyp_out;            // GEN: generated hypotheses [b][nh][vn]
+    float2 *hypv_out;           // GEN: optional keypoint-major copy [b][vn][nh]
+    int64_t hyp_sb, hyp_sv, hyp_sh;
     float *diag_hyp;            // GEN: optional copy [b][nh][vn][2]
     const int32_t *idxs;        // GEN: pixel pairs [b][nh][vn][2], or nullptr (counter RNG)
     int32_t *counts;            // counts[b*cnt_bs + v*cnt_v + h*cnt_h]
@@ -509,14 +513,30 @@ __device__ __forceinline__ float2 item_hyp(const VoteArgs &a, int b, int v, int 
             if (exact_intersect(e0.z, e0.w, e0.x, e0.y, e1.z, e1.w, e1.x, e1.y, &ox, &oy)) { x = ox; y = oy; }
             if (store) {
                 a.hyp_out[gid] = make_float2(x, y);
+                if (a.hypv_out) a.hypv_out[((int64_t)b * a.vn + v) * a.nh + h] = make_float2(x, y);
                 if (a.diag_hyp) { a.diag_hyp[gid * 2] = x; a.diag_hyp[gid * 2 + 1] = y; }
             }
         }
     } else if (hl) {
-        float2 q = a.hyp[((int64_t)b * a.nh + h) * a.vn + v];
+        float2 q = a.hyp[b * a.hyp_sb + v * a.hyp_sv + h * a.hyp_sh];
         x = q.x; y = q.y;
     }
     return make_float2(x, y);
+}
+
+// Hypotheses once per launch, one thread per (image, hypothesis, keypoint):
+// the pixel pair (the caller's idxs or the counter RNG, RV:553) and its
+// intersection (KU:11-49), stored in both layouts; images without a vote
+// (tn 0) are left alone.
+__global__ __launch_bounds__(256) void k_hyp_gen(VoteArgs a) {
+    const int64_t per = (int64_t)a.nh * a.vn;
+    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= per * a.b) return;
+    const int b = (int)(gid / per);
+    const int r = (int)(gid - b * per);
+    const int h = r / a.vn, v = r - h * a.vn;
+    const int n = a.tn_dev ? a.tn_dev[b] : a.tn_host;
+    if (n > 0) item_hyp<true, true>(a, b, v, h, true, n, true);
 }
 
 // wave w's share [lo, hi) of `total` items cut evenly over `nwaves` (32-bit: the callers keep total < 2^31)
@@ -605,22 +625,73 @@ struct ExactSlab<false> {
     __device__ __forceinline__ F4 get(int j) const { return e[j]; }
 };
 
-template <bool GEN, bool PREPPED>
-__device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, ExactSlab<PREPPED> &stagex, int b, int v, int hg, int ts,
-                                             int te, int n, int64_t rem_after, int64_t wave_total, int &nfix) {
+// LDS of one sub-chunk: fast operands and exact operands
+template <bool PREPPED>
+struct VoteSlab {
+    F4 stage[kVoteChunk];
+    ExactSlab<PREPPED> x;
+};
+// block-shared staging: the four quarter bounding boxes and exotic flags
+struct QuarterBoxes {
+    float4 box[4];
+    uint32_t exo[4];
+};
+
+//
+// SH (block-shared staging): the block's four waves take the same pixels
+// against four different hypothesis groups, so a sub-chunk is loaded and
+// staged once per block (one pixel per thread, double-buffered slabs, one
+// barrier per sub-chunk) instead of once per wave.  Its origin is the
+// sub-chunk's first pixel (known to every wave without a reduction); the
+// quarter boxes come through LDS.
+template <bool GEN, bool PREPPED, bool SH>
+__device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED> *slabs, QuarterBoxes *qbs, int &buf, int b, int v, int hg,
+                                             int ts, int te, int n, int64_t rem_after, int64_t wave_total, int &nfix) {
     const int lane = lane_id();
+    const int wid = SH ? (int)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave) : 0;
     // Issue priority from the work this wave still has (0..3): the SIMD's
     // arbiter otherwise favours the oldest wave, so equal shares finish
     // staggered and the last waves run alone; this keeps them level.
+    // (q = 4 * remaining / (wave_total + 1), compared instead of divided)
     auto set_prio = [&](int64_t remaining) {
-        const int64_t q = remaining * 4 / (wave_total + 1);
-        if (q >= 3) __builtin_amdgcn_s_setprio(3);
-        else if (q == 2) __builtin_amdgcn_s_setprio(2);
-        else if (q == 1) __builtin_amdgcn_s_setprio(1);
+        const int64_t r4 = remaining * 4, w1 = wave_total + 1;
+        if (r4 >= 3 * w1) __builtin_amdgcn_s_setprio(3);
+        else if (r4 >= 2 * w1) __builtin_amdgcn_s_setprio(2);
+        else if (r4 >= w1) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
     };
     const float tau = a.tau;
     constexpr float kBig = 3.0e38f;
+
+    // SH: the loads of a sub-chunk (this thread's pixel, the first pixel for
+    // the origin, the exotic flags); the first sub-chunk's are issued before
+    // the hypothesis generation so that the two memory round trips overlap
+    struct SubLoad {
+        F4 f0, e, q;
+        uint32_t exf;
+    };
+    auto load_sub = [&](int s0, int np) {
+        SubLoad L;
+        const int t = wid * kWave + lane;
+        L.f0 = pixel_exact<PREPPED>(a, b, v, s0);
+        L.e = F4{0.f, 0.f, 0.f, 0.f};
+        L.q = F4{__builtin_nanf(""), 0.f, 0.f, 0.f};
+        if (t < np) {
+            L.e = pixel_exact<PREPPED>(a, b, v, s0 + t);
+            if (PREPPED) {
+                const float4 f = a.pix[((int64_t)b * a.vn + v) * a.P + s0 + t];
+                L.q = F4{f.x, f.y, f.z, f.w};
+            }
+        }
+        L.exf = 0;
+        if (PREPPED) {
+            const uint32_t *exb = a.exotic + (int64_t)b * a.exotic_b;
+            L.exf = exb[s0 / kVoteChunk] | exb[(s0 + np - 1) / kVoteChunk];
+        }
+        return L;
+    };
+    SubLoad L;               // (loaded at the end of the previous sub-chunk: not live across its hot loop)
+    if (SH) L = load_sub(ts, min(kVoteChunk, te - ts));
 
     float2 he[kHypLane];     // exact hypotheses (the reference's operands)
     bool hf[kHypLane];       // decided by the fast test
@@ -630,7 +701,11 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, Exact
     for (int i = 0; i < kHypLane; ++i) {
         const int h = hg * kGroup + i * kWave + lane;
         const bool hl = h < a.nh;
+#ifndef PVVOTE_ABLATE_HYP
         he[i] = item_hyp<GEN, PREPPED>(a, b, v, h, hl, n, ts == 0);
+#else
+        he[i] = make_float2(300.f + 0.37f * lane + 0.11f * v, 200.f + 0.23f * i + 0.5f * hg);
+#endif
         const bool fin = isfinite(he[i].x) && isfinite(he[i].y);    // non-finite: never an inlier
         hxo[i] = hl && fin && hyp_exact_only(he[i].x, he[i].y);
         hf[i] = hl && fin && !hxo[i];
@@ -639,6 +714,75 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, Exact
 
     for (int s0 = ts; s0 < te; s0 += kVoteChunk) {
         const int np = min(kVoteChunk, te - s0);
+        VoteSlab<PREPPED> &S = slabs[SH ? buf : 0];
+        F4 *stage = S.stage;
+        ExactSlab<PREPPED> &stagex = S.x;
+        QuarterBoxes &QB = qbs[SH ? buf : 0];
+        if (SH) buf ^= 1;
+        float qxl = kBig, qxh = -kBig, qyl = kBig, qyh = -kBig;
+        float cxl = kBig, cxh = -kBig, cyl = kBig, cyh = -kBig;
+        float ox, oy, R;
+        bool slow = !a.fast;
+        if (SH) {
+            const int t = wid * kWave + lane;
+            ox = floorf(L.f0.x);
+            oy = floorf(L.f0.y);
+            if (!(fabsf(ox) <= 1.6e7f && fabsf(oy) <= 1.6e7f)) { ox = 0.f; oy = 0.f; }
+            F4 q = L.q;
+            float xl = kBig, xh = -kBig;
+            bool exo_p = false;
+            if (t < np) {
+                const F4 e = L.e;
+                if (!PREPPED) {
+                    const float4 f = prep_pixel(e.x, e.y, e.z, e.w);
+                    q = F4{f.x, f.y, f.z, f.w};
+                    exo_p = pixel_exotic(e.z, e.w);
+                }
+                stagex.put(t, e);
+                xl = e.x;
+                xh = e.x;
+            }
+            {
+                const float cx = q.x - ox, cy = q.y - oy;
+                const float k1 = fmaf(q.z, cx, q.w * cy);
+                const float k2 = fmaf(q.z, cy, -(q.w * cx));
+                stage[t] = F4{q.z, q.w, -k1, -k2};
+            }
+            if (wid * kWave < np) {
+                const float mn = wave_min(xl), mx = wave_max(xh);
+                float yn, yx;
+                if (PREPPED) {
+                    yn = bcast(q.y, 0);
+                    yx = bcast(q.y, min(kWave - 1, np - 1 - wid * kWave));
+                } else {
+                    const bool in = t < np;
+                    yn = wave_min(in ? q.y : kBig);
+                    yx = wave_max(in ? q.y : -kBig);
+                }
+                const uint32_t ex = __builtin_amdgcn_ballot_w64(exo_p) != 0;
+                if (lane == 0) {
+                    QB.box[wid] = make_float4(mn, mx, yn, yx);
+                    QB.exo[wid] = ex;
+                }
+            } else if (lane == 0) {
+                QB.box[wid] = make_float4(kBig, -kBig, kBig, -kBig);
+                QB.exo[wid] = 0;
+            }
+            __syncthreads();
+            uint32_t ex = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 Q = QB.box[k];
+                if (lane == k) { qxl = Q.x; qxh = Q.y; qyl = Q.z; qyh = Q.w; }
+                cxl = fminf(cxl, Q.x); cxh = fmaxf(cxh, Q.y);
+                cyl = fminf(cyl, Q.z); cyh = fmaxf(cyh, Q.w);
+                ex |= QB.exo[k];
+            }
+            slow |= (PREPPED ? L.exf : ex) != 0;
+            slow = __builtin_amdgcn_readfirstlane(slow);
+            const float ax = fmaxf(cxh - ox, ox - cxl), ay = fmaxf(cyh - oy, oy - cyl);
+            R = __builtin_amdgcn_sqrtf(fmaf(ax, ax, ay * ay)) * 1.00001f;
+        } else {
         F4 q4[kVoteChunk / kWave];
         float xl[kVoteChunk / kWave], xh[kVoteChunk / kWave];
         bool exo_p = false;
@@ -664,7 +808,6 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, Exact
             }
             q4[k] = q;
         }
-        bool slow = !a.fast;
         if (PREPPED) {
             const uint32_t *ex = a.exotic + (int64_t)b * a.exotic_b;
             slow |= (ex[s0 / kVoteChunk] | ex[(s0 + np - 1) / kVoteChunk]) != 0;
@@ -675,8 +818,6 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, Exact
         // per-quarter bounding boxes (lane k of qxl..qyh holds quarter k); the
         // compacted pixels are row-major, so a quarter's rows run from its
         // first pixel to its last (the API path takes arbitrary coordinates)
-        float qxl = kBig, qxh = -kBig, qyl = kBig, qyh = -kBig;
-        float cxl = kBig, cxh = -kBig, cyl = kBig, cyh = -kBig;
 #pragma unroll
         for (int k = 0; k < kVoteChunk / kWave; ++k) {
             if (k * kWave < np) {
@@ -696,9 +837,9 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, Exact
             }
         }
         const bool empty = !(cxl <= cxh) || !(cyl <= cyh);
-        const float ox = empty ? 0.f : floorf(cxl), oy = empty ? 0.f : floorf(cyl);
-        const float R = empty ? 0.f
-                              : __builtin_amdgcn_sqrtf(fmaf(cxh - ox, cxh - ox, (cyh - oy) * (cyh - oy))) * 1.00001f;
+        ox = empty ? 0.f : floorf(cxl);
+        oy = empty ? 0.f : floorf(cyl);
+        R = empty ? 0.f : __builtin_amdgcn_sqrtf(fmaf(cxh - ox, cxh - ox, (cyh - oy) * (cyh - oy))) * 1.00001f;
         // stage the fast operands (ux, uy, -k1, -k2)
 #pragma unroll
         for (int k = 0; k < kVoteChunk / kWave; ++k) {
@@ -709,6 +850,7 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, Exact
             stage[k * kWave + lane] = F4{q.z, q.w, -k1, -k2};
         }
         __builtin_amdgcn_wave_barrier();
+        }
         // lane constants of this sub-chunk
         float hx[kHypLane], hy[kHypLane], Bv[kHypLane], gd[kHypLane];
 #pragma unroll
@@ -789,7 +931,11 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, Exact
             };
             // the slab past np holds NaN pixels (never counted, never in the
             // band), so the loop runs whole 8-pixel iterations
+#ifdef PVVOTE_ABLATE_LOOP
+            const int nit = 0;
+#else
             const int nit = (np + 7) >> 3;
+#endif
             F4 a0 = stage[0], a1 = stage[1], a2 = stage[2], a3 = stage[3];
             for (int it = 0; it < nit; ++it) {
                 const int j = it * 8;
@@ -834,34 +980,45 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, F4 *stage, Exact
                 for (int i = 0; i < kHypLane; ++i) cnt[i] += exact_vote(e.z, e.w, e.x, e.y, he[i].x, he[i].y, a.thr);
             }
         }
-        __builtin_amdgcn_wave_barrier();
+        if (!SH) __builtin_amdgcn_wave_barrier();
+        if (SH && s0 + kVoteChunk < te) L = load_sub(s0 + kVoteChunk, min(kVoteChunk, te - s0 - kVoteChunk));
     }
     int32_t *cp = a.counts + (int64_t)b * a.cnt_bs + (int64_t)v * a.cnt_v;
 #pragma unroll
     for (int i = 0; i < kHypLane; ++i) {
         const int h = hg * kGroup + i * kWave + lane;
+#ifndef PVVOTE_ABLATE_ATOMIC
         if (h < a.nh && cnt[i]) atomicAdd(&cp[(int64_t)h * a.cnt_h], cnt[i]);
+#else
+        if (h < a.nh && cnt[i] == 0x7fffffff) cp[0] = 1;
+#endif
     }
 }
 
 // Balanced persistent waves: the (image, keypoint, hypothesis group, pixel)
 // work space is linearised with pixels fastest and cut into equal contiguous
 // ranges, one per wave, so every wave does the same number of pixel steps and
-// generates each group's hypotheses once per range.
-template <bool GEN, bool PREPPED>
+// generates each group's hypotheses once per range.  SH: the unit is a block
+// (its four waves = four consecutive hypothesis groups on the same pixels),
+// the space is (image, keypoint, group of four groups, pixel); needs
+// hgn % 4 == 0 (hn a multiple of 512).
+template <bool GEN, bool PREPPED, bool SH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) void k_vote_count(VoteArgs a) {
     const int wave = uniform((int)(blockIdx.x * 4 + threadIdx.x / 64));
-    const int64_t nwaves = (int64_t)gridDim.x * 4;
+    const int unit = SH ? (int)blockIdx.x : wave;
+    const int64_t nunits = SH ? (int64_t)gridDim.x : (int64_t)gridDim.x * 4;
+    const int gpu = SH ? 4 : 1;           // hypothesis groups per unit
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    __shared__ F4 stage_all[4][kVoteChunk];
-    __shared__ ExactSlab<PREPPED> stagex_all[4];
-    F4 *stage = stage_all[threadIdx.x / 64];
-    ExactSlab<PREPPED> &stagex = stagex_all[threadIdx.x / 64];
+    __shared__ VoteSlab<PREPPED> slab_all[SH ? 2 : 4];
+    __shared__ QuarterBoxes qb_all[SH ? 2 : 1];
+    VoteSlab<PREPPED> *slabs = SH ? slab_all : slab_all + threadIdx.x / 64;
+    int buf = 0;
+    const int ggn = a.hgn / gpu;          // unit groups per keypoint
     // 32-bit index math (the host splits launches so that the work stays < 2^31)
     uint32_t total = 0;
-    for (int b = 0; b < a.b; ++b) total += (uint32_t)(a.vn * a.hgn) * (uint32_t)(a.tn_dev ? a.tn_dev[b] : a.tn_host);
+    for (int b = 0; b < a.b; ++b) total += (uint32_t)(a.vn * ggn) * (uint32_t)(a.tn_dev ? a.tn_dev[b] : a.tn_host);
     uint32_t lo, hi;
-    even_share(total, (uint32_t)nwaves, (uint32_t)wave, &lo, &hi);
+    even_share(total, (uint32_t)nunits, (uint32_t)unit, &lo, &hi);
     const int64_t wave_total = hi - lo;
     int nfix = 0, nseg = 0;   // diagnostics (trace)
     // walk the segments of [lo, hi)
@@ -869,15 +1026,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     uint32_t base = 0;
     while (lo < hi) {
         const int n = a.tn_dev ? a.tn_dev[b] : a.tn_host;
-        const uint32_t span = (uint32_t)(a.vn * a.hgn) * (uint32_t)n;
+        const uint32_t span = (uint32_t)(a.vn * ggn) * (uint32_t)n;
         if (lo >= base + span) { base += span; ++b; continue; }
         const uint32_t r = lo - base;
-        const int g = (int)(r / (uint32_t)n);               // (v, hg) group index
+        const int g = (int)(r / (uint32_t)n);               // (v, unit group) index
         const int ts = (int)(r - (uint32_t)g * n);
         const int te = (int)min((uint32_t)n, ts + (hi - lo));
-        const int v = g / a.hgn, hg = g - v * a.hgn;
-        vote_segment<GEN, PREPPED>(a, stage, stagex, uniform(b), uniform(v), uniform(hg), uniform(ts), uniform(te),
-                                   n, (int64_t)(hi - lo) - (te - ts), wave_total, nfix);
+        const int v = g / ggn, gg = g - v * ggn;
+        const int hg = SH ? gg * 4 + (int)__builtin_amdgcn_readfirstlane(threadIdx.x / 64) : gg;
+        vote_segment<GEN, PREPPED, SH>(a, slabs, qb_all, buf, uniform(b), uniform(v), uniform(hg), uniform(ts), uniform(te), n,
+                                       (int64_t)(hi - lo) - (te - ts), wave_total, nfix);
         lo += te - ts;
         ++nseg;
     }
@@ -1782,12 +1940,26 @@ void fast_constants(float thr, VoteArgs *va) {
 int vote_grid_steps(int64_t pixel_steps, const void *kernel) {
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0) per_cu = 4;
+    static const int cap_env = getenv("PVVOTE_VOTE_PER_CU") ? atoi(getenv("PVVOTE_VOTE_PER_CU")) : 0;   // A/B (temporary)
+    if (cap_env > 0 && cap_env < per_cu) per_cu = cap_env;
     int64_t cap = (int64_t)cu_count() * per_cu;
     int64_t need = (pixel_steps / 128 + 3) / 4;
     return (int)(need < 1 ? 1 : (need < cap ? need : cap));
 }
 
 uint64_t *g_vote_trace = nullptr;   // debug hook (pv_debug_set_vote_trace)
+
+// the vote launch: block-shared staging when the groups come in fours
+template <bool GEN, bool PREPPED>
+void launch_vote(const VoteArgs &va, int64_t pixel_steps, hipStream_t s) {
+    static const bool no_sh = getenv("PVVOTE_NO_SH") != nullptr;   // A/B switch (temporary)
+    if (va.hgn % 4 == 0 && !no_sh)
+        k_vote_count<GEN, PREPPED, true>
+            <<<vote_grid_steps(pixel_steps, (const void *)k_vote_count<GEN, PREPPED, true>), 256, 0, s>>>(va);
+    else
+        k_vote_count<GEN, PREPPED, false>
+            <<<vote_grid_steps(pixel_steps, (const void *)k_vote_count<GEN, PREPPED, false>), 256, 0, s>>>(va);
+}
 
 struct Launch {
     int kind;
@@ -1874,6 +2046,15 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
     va.b = b; va.vn = vn; va.nh = nh; va.hgn = (nh + kGroup - 1) / kGroup;
     fast_constants(prm->inlier_thresh, &va);
     va.trace = g_vote_trace;
+    static const bool gen_in_vote = getenv("PVVOTE_GEN_IN_VOTE") != nullptr;   // A/B switch (temporary)
+    // hypotheses first (one kernel for the batch), keypoint-major for the vote
+    if (!gen_in_vote) {
+        va.hypv_out = w.hypv;
+        const int64_t nt = (int64_t)b * nh * vn;
+        k_hyp_gen<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(va);
+        if ((r = last())) return r;
+        va.hyp = w.hypv; va.hyp_sb = (int64_t)vn * nh; va.hyp_sv = nh; va.hyp_sh = 1;
+    }
     if (dg.ev_vote_begin) {
         hipError_t e = hipEventRecord((hipEvent_t)dg.ev_vote_begin, s);
         if (e != hipSuccess) return rc(e);
@@ -1896,7 +2077,12 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
         if (vc.idxs) vc.idxs += (int64_t)b0 * nh * vn * 2;
         vc.counts += (int64_t)b0 * va.cnt_bs;
         vc.tn_dev += b0;
-        k_vote_count<true, true><<<vote_grid_steps(nb * per_img, (const void *)k_vote_count<true, true>), 256, 0, s>>>(vc);
+        if (gen_in_vote) {
+            launch_vote<true, true>(vc, nb * per_img, s);
+        } else {
+            vc.hyp += b0 * vc.hyp_sb;
+            launch_vote<false, true>(vc, nb * per_img, s);
+        }
         if ((r = last())) return r;
     }
     if (dg.ev_vote_end) return rc(hipEventRecord((hipEvent_t)dg.ev_vote_end, s));
@@ -2012,15 +2198,14 @@ int pv_vote_counts(const float *direct, const float *coords, const float *hypo, 
     VoteArgs va{};
     va.coords = (const float2 *)coords; va.P = tn;
     va.raw = (const float2 *)direct; va.raw_v = 1; va.raw_t = vn;
-    va.hyp = (const float2 *)hypo;
+    va.hyp = (const float2 *)hypo; va.hyp_sb = 0; va.hyp_sv = 1; va.hyp_sh = vn;
     va.counts = counts; va.cnt_bs = 0; va.cnt_v = 1; va.cnt_h = vn;
     va.tn_dev = nullptr; va.tn_host = tn;
     va.b = 1; va.vn = vn; va.nh = hn; va.hgn = (hn + kGroup - 1) / kGroup;
     fast_constants(inlier_thresh, &va);
     if (tn == 0) return PV_OK;
     if ((int64_t)vn * va.hgn * tn >= (1ll << 31)) return PV_EINVAL;   // the kernel's 32-bit work index
-    k_vote_count<false, false><<<vote_grid_steps((int64_t)vn * va.hgn * tn, (const void *)k_vote_count<false, false>),
-                                 256, 0, s>>>(va);
+    launch_vote<false, false>(va, (int64_t)vn * va.hgn * tn, s);
     return last();
 }
 
