@@ -426,13 +426,17 @@ __global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int 
 // K4: hypotheses (KU:11-49) + fused vote/count.
 // counts[b][v][h] += #{t : inlier(h, v, t)}.
 //
-// Work item = (image, keypoint v, chunk of 256 pixels, group of 64
-// hypotheses); one item per wave, items strided over a fixed grid.  Lane =
-// hypothesis: each wave generates its own 64 hypotheses (pixel pairs from the
-// caller or the counter RNG, RV:553) and the chunk-0 wave of each group stores
-// them for the refine stage.  The pixels are wave-uniform and come through
-// scalar loads, so a pixel costs no vector instruction besides the test, and
-// the per-lane inlier count is one v_addc on the compare's VCC.
+// k_hyp_gen makes every hypothesis once (pixel pairs from the caller or the
+// counter RNG, RV:553) and stores it in the reference layout (refine stage,
+// diagnostics) and keypoint-major (the vote's coalesced reads).
+//
+// k_vote_count: lane = hypothesis (kHypLane = 2 per lane, groups of 128 per
+// wave); the (image, keypoint, group, pixel) space is cut into equal
+// contiguous ranges over persistent units.  With hn a multiple of 512 a unit
+// is a block whose four waves take four groups against the same pixels, which
+// the block stages once per 256-pixel sub-chunk in LDS; every wave then reads
+// a pixel's four fast operands with one broadcast ds_read_b128, and the
+// per-lane inlier count is one v_addc on the compare's VCC.
 //
 // The test (fast path) works in the pixel's rotated frame: with u the unit
 // predicted direction and d = h - c,
@@ -475,7 +479,6 @@ struct VoteArgs {
     uint64_t seed;
     int32_t P, raw_v, raw_t, exotic_b, cnt_v, cnt_h, cnt_bs;
     int32_t tn_host, b, vn, nh, hgn, fast;
-    int32_t b_base;             // first image of this launch (RNG keys stay per global image)
     float thr, tau, gzf, gzr;
     uint64_t *trace;            // debug: per-wave (start, end) s_memrealtime stamps, or nullptr
 };
@@ -504,7 +507,7 @@ __device__ __forceinline__ float2 item_hyp(const VoteArgs &a, int b, int v, int 
                 t0 = min(max(a.idxs[gid * 2], 0), n - 1);
                 t1 = min(max(a.idxs[gid * 2 + 1], 0), n - 1);
             } else {
-                const uint64_t key = (uint64_t)gid + (uint64_t)a.b_base * a.nh * a.vn;
+                const uint64_t key = (uint64_t)gid;
                 t0 = rand_index(a.seed, key * 2, n);
                 t1 = rand_index(a.seed, key * 2 + 1, n);
             }
@@ -644,7 +647,7 @@ struct QuarterBoxes {
 // barrier per sub-chunk) instead of once per wave.  Its origin is the
 // sub-chunk's first pixel (known to every wave without a reduction); the
 // quarter boxes come through LDS.
-template <bool GEN, bool PREPPED, bool SH>
+template <bool PREPPED, bool SH>
 __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED> *slabs, QuarterBoxes *qbs, int &buf, int b, int v, int hg,
                                              int ts, int te, int n, int64_t rem_after, int64_t wave_total, int &nfix) {
     const int lane = lane_id();
@@ -702,7 +705,7 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
         const int h = hg * kGroup + i * kWave + lane;
         const bool hl = h < a.nh;
 #ifndef PVVOTE_ABLATE_HYP
-        he[i] = item_hyp<GEN, PREPPED>(a, b, v, h, hl, n, ts == 0);
+        he[i] = item_hyp<false, PREPPED>(a, b, v, h, hl, n, false);
 #else
         he[i] = make_float2(300.f + 0.37f * lane + 0.11f * v, 200.f + 0.23f * i + 0.5f * hg);
 #endif
@@ -1002,7 +1005,7 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
 // (its four waves = four consecutive hypothesis groups on the same pixels),
 // the space is (image, keypoint, group of four groups, pixel); needs
 // hgn % 4 == 0 (hn a multiple of 512).
-template <bool GEN, bool PREPPED, bool SH>
+template <bool PREPPED, bool SH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) void k_vote_count(VoteArgs a) {
     const int wave = uniform((int)(blockIdx.x * 4 + threadIdx.x / 64));
     const int unit = SH ? (int)blockIdx.x : wave;
@@ -1034,7 +1037,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         const int te = (int)min((uint32_t)n, ts + (hi - lo));
         const int v = g / ggn, gg = g - v * ggn;
         const int hg = SH ? gg * 4 + (int)__builtin_amdgcn_readfirstlane(threadIdx.x / 64) : gg;
-        vote_segment<GEN, PREPPED, SH>(a, slabs, qb_all, buf, uniform(b), uniform(v), uniform(hg), uniform(ts), uniform(te), n,
+        vote_segment<PREPPED, SH>(a, slabs, qb_all, buf, uniform(b), uniform(v), uniform(hg), uniform(ts), uniform(te), n,
                                        (int64_t)(hi - lo) - (te - ts), wave_total, nfix);
         lo += te - ts;
         ++nseg;
@@ -1937,11 +1940,10 @@ void fast_constants(float thr, VoteArgs *va) {
 // persistent vote grid: every block resident at once (the occupancy limit of
 // the kernel: LDS slabs, registers), fewer when the work is small (>= ~128
 // pixel steps per wave)
-int vote_grid_steps(int64_t pixel_steps, const void *kernel) {
+int vote_grid_steps(int64_t pixel_steps, const void *kernel, int max_per_cu = 1 << 30) {
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0) per_cu = 4;
-    static const int cap_env = getenv("PVVOTE_VOTE_PER_CU") ? atoi(getenv("PVVOTE_VOTE_PER_CU")) : 0;   // A/B (temporary)
-    if (cap_env > 0 && cap_env < per_cu) per_cu = cap_env;
+    per_cu = std::min(per_cu, max_per_cu);
     int64_t cap = (int64_t)cu_count() * per_cu;
     int64_t need = (pixel_steps / 128 + 3) / 4;
     return (int)(need < 1 ? 1 : (need < cap ? need : cap));
@@ -1950,15 +1952,16 @@ int vote_grid_steps(int64_t pixel_steps, const void *kernel) {
 uint64_t *g_vote_trace = nullptr;   // debug hook (pv_debug_set_vote_trace)
 
 // the vote launch: block-shared staging when the groups come in fours
-template <bool GEN, bool PREPPED>
+// (SH: at most 4 of its 5 resident blocks per CU, which measured faster for
+// one launch and leaves room for a concurrent image's small kernels)
+template <bool PREPPED>
 void launch_vote(const VoteArgs &va, int64_t pixel_steps, hipStream_t s) {
-    static const bool no_sh = getenv("PVVOTE_NO_SH") != nullptr;   // A/B switch (temporary)
-    if (va.hgn % 4 == 0 && !no_sh)
-        k_vote_count<GEN, PREPPED, true>
-            <<<vote_grid_steps(pixel_steps, (const void *)k_vote_count<GEN, PREPPED, true>), 256, 0, s>>>(va);
+    if (va.hgn % 4 == 0)
+        k_vote_count<PREPPED, true>
+            <<<vote_grid_steps(pixel_steps, (const void *)k_vote_count<PREPPED, true>, 4), 256, 0, s>>>(va);
     else
-        k_vote_count<GEN, PREPPED, false>
-            <<<vote_grid_steps(pixel_steps, (const void *)k_vote_count<GEN, PREPPED, false>), 256, 0, s>>>(va);
+        k_vote_count<PREPPED, false>
+            <<<vote_grid_steps(pixel_steps, (const void *)k_vote_count<PREPPED, false>), 256, 0, s>>>(va);
 }
 
 struct Launch {
@@ -2046,15 +2049,15 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
     va.b = b; va.vn = vn; va.nh = nh; va.hgn = (nh + kGroup - 1) / kGroup;
     fast_constants(prm->inlier_thresh, &va);
     va.trace = g_vote_trace;
-    static const bool gen_in_vote = getenv("PVVOTE_GEN_IN_VOTE") != nullptr;   // A/B switch (temporary)
-    // hypotheses first (one kernel for the batch), keypoint-major for the vote
-    if (!gen_in_vote) {
-        va.hypv_out = w.hypv;
+    // hypotheses first, once each (one kernel for the batch); the vote
+    // kernel reads them keypoint-major
+    va.hypv_out = w.hypv;
+    {
         const int64_t nt = (int64_t)b * nh * vn;
         k_hyp_gen<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(va);
         if ((r = last())) return r;
-        va.hyp = w.hypv; va.hyp_sb = (int64_t)vn * nh; va.hyp_sv = nh; va.hyp_sh = 1;
     }
+    va.hyp = w.hypv; va.hyp_sb = (int64_t)vn * nh; va.hyp_sv = nh; va.hyp_sh = 1;
     if (dg.ev_vote_begin) {
         hipError_t e = hipEventRecord((hipEvent_t)dg.ev_vote_begin, s);
         if (e != hipSuccess) return rc(e);
@@ -2068,21 +2071,13 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
         VoteArgs vc = va;
         const int nb = std::min(chunk, b - b0);
         vc.b = nb;
-        vc.b_base = b0;
         vc.pix += (int64_t)b0 * vn * P;
         vc.pex += (int64_t)b0 * vn * P;
         vc.exotic += (int64_t)b0 * va.exotic_b;
-        vc.hyp_out += (int64_t)b0 * nh * vn;
-        if (vc.diag_hyp) vc.diag_hyp += (int64_t)b0 * nh * vn * 2;
-        if (vc.idxs) vc.idxs += (int64_t)b0 * nh * vn * 2;
+        vc.hyp += b0 * vc.hyp_sb;
         vc.counts += (int64_t)b0 * va.cnt_bs;
         vc.tn_dev += b0;
-        if (gen_in_vote) {
-            launch_vote<true, true>(vc, nb * per_img, s);
-        } else {
-            vc.hyp += b0 * vc.hyp_sb;
-            launch_vote<false, true>(vc, nb * per_img, s);
-        }
+        launch_vote<true>(vc, nb * per_img, s);
         if ((r = last())) return r;
     }
     if (dg.ev_vote_end) return rc(hipEventRecord((hipEvent_t)dg.ev_vote_end, s));
@@ -2205,7 +2200,7 @@ int pv_vote_counts(const float *direct, const float *coords, const float *hypo, 
     fast_constants(inlier_thresh, &va);
     if (tn == 0) return PV_OK;
     if ((int64_t)vn * va.hgn * tn >= (1ll << 31)) return PV_EINVAL;   // the kernel's 32-bit work index
-    launch_vote<false, false>(va, (int64_t)vn * va.hgn * tn, s);
+    launch_vote<false>(va, (int64_t)vn * va.hgn * tn, s);
     return last();
 }
 
