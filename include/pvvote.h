@@ -71,6 +71,13 @@ int pv_voting_for_hypothesis(const float *direct, const float *coords, const flo
                              int32_t tn, int32_t vn, int32_t hn, float inlier_thresh, int32_t mode,
                              pv_stream_t stream);
 
+/* the same with caller-owned scratch (no allocation on the stream): workspace of at least
+ * pv_voting_for_hypothesis_workspace_size(tn, vn, hn) bytes, device memory, 256-byte aligned. */
+size_t pv_voting_for_hypothesis_workspace_size(int32_t tn, int32_t vn, int32_t hn);
+int pv_voting_for_hypothesis_ws(const float *direct, const float *coords, const float *hypo, uint8_t *inliers,
+                                int32_t tn, int32_t vn, int32_t hn, float inlier_thresh, int32_t mode,
+                                void *workspace, size_t workspace_bytes, pv_stream_t stream);
+
 /* replaces generate_hypothesis_vanishing_point (BND:64-75 -> KU:231-266); hypo f32 [hn,vn,3]. */
 int pv_generate_hypothesis_vp(const float *direct, const float *coords, const int32_t *idxs, float *hypo,
                               int32_t tn, int32_t vn, int32_t hn, pv_stream_t stream);

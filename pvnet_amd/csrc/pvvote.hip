@@ -1557,6 +1557,11 @@ __global__ __launch_bounds__(256) void k_generate_api(const float *direct, const
 constexpr int kBytePix = 8;
 constexpr int kByteWin = kWave * kBytePix;      // bytes of a row per segment
 constexpr int kByteHB = 64;                      // hypothesis records per batch
+constexpr uint32_t kQueuePerWave = 128;          // band pairs a wave queues for its end (LDS)
+
+#ifdef PVVOTE_TRACE_U1
+__device__ uint64_t *g_btrace;      // debug build only: per-wave phase stamps of k_vote_bytes
+#endif
 
 struct ByteArgs {
     const float4 *prep;    // [vn][tn] (ux, uy, cx, cy), see k_prep_api
@@ -1606,17 +1611,33 @@ __global__ __launch_bounds__(256) void k_prep_api(const float *direct, const flo
 }
 
 // rows [i0, i1) (i1 - i0 <= kByteHB) of keypoint v, class c, window w
+// Issue priority from the rows a wave still has (0..3), as in vote_segment:
+// otherwise the SIMD favours its oldest wave, equal shares finish staggered
+// and the last waves of each SIMD run alone at a fraction of the issue rate.
+__device__ __forceinline__ void prio_by_remaining(uint32_t remaining, uint32_t total) {
+    const uint64_t r4 = (uint64_t)remaining * 4, w1 = (uint64_t)total + 1;
+    if (r4 >= 3 * w1) __builtin_amdgcn_s_setprio(3);
+    else if (r4 >= 2 * w1) __builtin_amdgcn_s_setprio(2);
+    else if (r4 >= w1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
+
 template <int MODE>
-__device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, int v, int c, int w, int i0, int i1) {
+__device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint8_t *band8, int v, int c, int w,
+                                               int i0, int i1, uint32_t rem_after, uint32_t wave_total,
+                                               uint2 *wq, uint32_t &qn) {
+    const uint32_t qcap = a.dbg == 4 ? 1u : kQueuePerWave;   // (dbg 4: test hook, a full queue)
     const int lane = lane_id();
-    const float tau = a.tau;
+    const float ntau = -a.tau;
     const int nh = i1 - i0;
     const int h0 = c + 8 * i0;                                  // rows h0 + 8i, i < nh
     const int64_t R0 = ((int64_t)h0 * a.vn + v) * a.tn;
     const int s = (int)(R0 & 7);
     const int tb = kByteWin * w - s + kBytePix * lane;          // lane's first pixel
     const int64_t rstep = (int64_t)8 * a.vn * a.tn;             // R(h + 8) - R(h)
-    uint8_t *orow = a.out + R0 - s + (int64_t)kByteWin * w + kBytePix * lane;   // 8-byte aligned
+    // row i's word of this lane: wave-uniform offset (SGPRs) + 32-bit lane offset
+    const int64_t obase = R0 - s + (int64_t)kByteWin * w;
+    const uint32_t loff = kBytePix * lane;
 
     // ---- operands: all loads issued together ----
     float2 hq = make_float2(0.f, 0.f);
@@ -1641,9 +1662,10 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, int 
         if (fu[j] != 0.f || fv[j] != 0.f) okmask |= 1u << j;    // votes at all
     }
     const bool slow = __builtin_amdgcn_readfirstlane(!a.fast || __builtin_amdgcn_ballot_w64(exo) != 0);
-    // origin: an integer point at the first voting pixel; R >= |c - o| over the voting pixels
+    // origin: an integer point at the first voting pixel; the voting pixels'
+    // bounding box relative to it (R >= |c - o|, and D >= |h - c| per row)
     const uint64_t anyok = __builtin_amdgcn_ballot_w64(okmask != 0);
-    float ox = 0.f, oy = 0.f, Rw = 0.f;
+    float ox = 0.f, oy = 0.f, Rw = 0.f, bxl = 0.f, bxh = 0.f, byl = 0.f, byh = 0.f;
     if (anyok) {
         const int l0 = __builtin_ctzll(anyok);
         const int j0 = __builtin_ctz(__builtin_amdgcn_readlane(okmask, l0));
@@ -1653,15 +1675,21 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, int 
             if (j == j0) { fx = fk1[j]; fy = fk2[j]; }
         ox = floorf(bcast(fx, l0));
         oy = floorf(bcast(fy, l0));
-        float r2 = 0.f;
+        float xl = 3.0e38f, xh = -3.0e38f, yl = 3.0e38f, yh = -3.0e38f;
 #pragma unroll
         for (int j = 0; j < kBytePix; ++j)
-            if (okmask >> j & 1) r2 = fmaxf(r2, fmaf(fk1[j] - ox, fk1[j] - ox, (fk2[j] - oy) * (fk2[j] - oy)));
-        Rw = __builtin_amdgcn_sqrtf(wave_max(r2)) * 1.00001f;
+            if (okmask >> j & 1) {
+                xl = fminf(xl, fk1[j] - ox); xh = fmaxf(xh, fk1[j] - ox);
+                yl = fminf(yl, fk2[j] - oy); yh = fmaxf(yh, fk2[j] - oy);
+            }
+        bxl = wave_min(xl); bxh = wave_max(xh);
+        byl = wave_min(yl); byh = wave_max(yh);
+        const float ax = fmaxf(-bxl, bxh), ay = fmaxf(-byl, byh);
+        Rw = __builtin_amdgcn_sqrtf(fmaf(ax, ax, ay * ay)) * 1.00001f;
     }
     // fast operands (ux, uy, -k1, -k2) relative to the origin, in place;
-    // pixels that never vote get u = 0, -k1 = -1e30: z = -1e30 tau, far
-    // below the band, for every finite h'
+    // pixels that never vote get u = 0, -k1 = -1e30: -z = 1e30 tau, far
+    // above the band, for every finite h'
 #pragma unroll
     for (int j = 0; j < kBytePix; ++j) {
         const bool ok = okmask >> j & 1;
@@ -1684,7 +1712,10 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, int 
             if (!xo && !slow) {
                 const float hx = hq.x - ox, hy = hq.y - oy;
                 const float B = (__builtin_amdgcn_sqrtf(fmaf(hx, hx, hy * hy)) + Rw) * 1.00001f + 1e-30f;
-                rec = F4{hx, hy, (a.gzf + a.gzr) * B * 1.00001f, 0.f};
+                const float dx = fmaxf(fabsf(hx - bxl), fabsf(hx - bxh));
+                const float dy = fmaxf(fabsf(hy - byl), fabsf(hy - byh));
+                const float D = fmaf(__builtin_amdgcn_sqrtf(fmaf(dx, dx, dy * dy)), 1.00001f, B * 1e-6f);
+                rec = F4{hx, hy, fmaf(a.gzr, D, a.gzf * B) * 1.00001f, 0.f};
             }
         }
         flagged = __builtin_amdgcn_ballot_w64(lane < nh && rec.w != 0.f);
@@ -1693,17 +1724,8 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, int 
         __builtin_amdgcn_wave_barrier();
     }
 
-    // the reference's decision of pixel j against row h (rare paths)
-    auto exact_at = [&](int j, int h) {
-        int t = tb + j;
-        asm volatile("" : "+v"(t));   // keep the address math here: not hoisted into live registers
-        const float2 q = *(const float2 *)(a.hypo + ((int64_t)h * a.vn + v) * 2);
-        const float2 cc = *(const float2 *)(a.coords + (int64_t)t * 2);
-        const float2 d = *(const float2 *)(a.direct + ((int64_t)t * a.vn + v) * 2);
-        return exact_vote(d.x, d.y, cc.x, cc.y, q.x, q.y, a.thr);
-    };
-    auto store = [&](uint8_t *p, uint32_t lo, uint32_t hi) {
-        if (vmask == 0xffu) {
+    auto store = [&](uint8_t *p, uint32_t lo, uint32_t hi, auto partial) {
+        if (!decltype(partial)::value || vmask == 0xffu) {
             if (MODE == PV_VOTE_DENSE) {
                 *(uint2 *)p = make_uint2(lo, hi);
             } else {
@@ -1722,96 +1744,189 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, int 
             }
         }
     };
-    // byte k of perm(hi, lo, sel) = byte sel_k of {hi, lo}: the sign bytes of four z's
-    constexpr uint32_t kSel01 = 0x0c0c0703u;   // z0.b3 -> b0, z1.b3 -> b1 (perm(z1, z0))
+    // inlier bytes from the signs of nz = -z: v_perm's selectors 9 / 11
+    // replicate the sign bit of its second / first operand into a byte, 12 is 0
+    constexpr uint32_t kSgn01 = 0x0c0c0b09u;   // sign(z0) -> b0, sign(z1) -> b1
     constexpr uint32_t kSel23 = 0x05040100u;   // p01.b0,b1 -> b0,b1; p23.b0,b1 -> b2,b3
     auto pack4 = [&](float z0, float z1, float z2, float z3) {
-        const uint32_t p01 = __builtin_amdgcn_perm(__float_as_uint(z1), __float_as_uint(z0), kSel01);
-        const uint32_t p23 = __builtin_amdgcn_perm(__float_as_uint(z3), __float_as_uint(z2), kSel01);
-        const uint32_t sg = __builtin_amdgcn_perm(p23, p01, kSel23);
-        return (~sg & 0x80808080u) >> 7;            // 1 where z > 0 (band pairs are fixed below)
+        const uint32_t p01 = __builtin_amdgcn_perm(__float_as_uint(z1), __float_as_uint(z0), kSgn01);
+        const uint32_t p23 = __builtin_amdgcn_perm(__float_as_uint(z3), __float_as_uint(z2), kSgn01);
+        return __builtin_amdgcn_perm(p23, p01, kSel23) & 0x01010101u;   // 1 where z > 0 (band pairs fixed below)
     };
-
-    auto zrow = [&](const F4 &rec, float z[kBytePix]) {
+    // nz = -z = x' (-tau) + |y'|, and min |nz| for the band check
+    auto zrow = [&](const F4 &rec, float nz[kBytePix]) {
         float m = 3.0e38f;
 #pragma unroll
         for (int j = 0; j < kBytePix; ++j) {
             const float xr = fmaf(fu[j], rec.x, fmaf(fv[j], rec.y, fk1[j]));
             const float yr = fmaf(fu[j], rec.y, fmaf(-fv[j], rec.x, fk2[j]));
-            z[j] = fmaf(xr, tau, -fabsf(yr));
-            m = fminf(m, fabsf(z[j]));
+            nz[j] = fmaf(xr, ntau, fabsf(yr));
+            m = fminf(m, fabsf(nz[j]));
         }
         return m;
     };
 
     // Hot loop: the fast decision of every pair, one 8-byte store per row.
-    // Rows with a pair inside the band and rows outside the fast domain are
-    // deferred to the exact pass below, which writes them instead -- the hot
-    // loop carries no exact-sequence code.  Waves holding a partial word (row
-    // ends) run the same loop with per-lane byte stores.
-    uint64_t dmask = flagged;                           // deferred rows (nh <= 64)
-    auto rows = [&](auto partial) {
-        F4 rec = recs[0];
-        uint8_t *p = orow;
-        for (int i = 0; i < nh; ++i) {
-            const F4 nrec = recs[min(i + 1, kByteHB - 1)];    // next record, one iteration ahead
-            float z[kBytePix];
-            const float m = zrow(rec, z);
-            const uint64_t hit = __builtin_amdgcn_ballot_w64(m <= rec.z);   // flagged rows: rec.z = inf
-            const uint32_t lo = pack4(z[0], z[1], z[2], z[3]), hi = pack4(z[4], z[5], z[6], z[7]);
-            if constexpr (MODE == PV_VOTE_DENSE && !decltype(partial)::value) {
-                // dense: store every row; a deferred row is rewritten by the exact pass
-                // (same lane, same address: program order)
-                *(uint2 *)p = make_uint2(lo, hi);
-                dmask |= (uint64_t)(hit != 0) << i;
-            } else {
-                if (hit) dmask |= 1ull << i;
-                else store(p, lo, hi);
-            }
-            p += rstep;
-            rec = nrec;
+    // A row with a pair inside the band records which (an 8-bit mask per lane
+    // in LDS) and its word is stored with those bytes as the fast guess
+    // (dense) or left out (OR); the exact pass rewrites just those bytes.
+    // Flagged rows (outside the fast domain) are decided whole by the exact
+    // pass.  Waves holding a partial word (row ends) use byte stores.
+    // Queue this lane's band pairs of row i (bits of bm) in the wave's LDS
+    // queue, decided at the wave's end (fix_queued): a wave prefix of the
+    // per-lane counts (<= 8, four ballots).  False when the queue is full
+    // (entries that fit are still written: deciding a pair twice is harmless,
+    // both give the reference's byte).
+    auto enqueue = [&](uint32_t bm, int i) {
+        const uint32_t n = __builtin_popcount(bm);
+        uint32_t pre = 0, tot = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t m = __builtin_amdgcn_ballot_w64((n >> k) & 1u);
+            pre += (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << k;
+            tot += (uint32_t)__builtin_popcountll(m) << k;
         }
+        const uint32_t base = qn;
+        qn = min(base + tot, qcap);
+        const uint32_t r = (uint32_t)((h0 + 8 * i) * a.vn + v);
+        uint32_t k = base + pre;
+#pragma unroll
+        for (int j = 0; j < kBytePix; ++j) {
+            if (bm >> j & 1) {
+                if (k < qcap) wq[k] = make_uint2(r, (uint32_t)(tb + j));
+                ++k;
+            }
+        }
+        return base + tot <= qcap;
+    };
+    uint64_t dmask = 0;                                 // rows with exact work in this kernel (nh <= 64)
+    uint32_t lof = loff;                                // (loop-carried through the asm below: no copies)
+    auto row = [&](const F4 &rec, int i, auto partial) {
+        float nz[kBytePix];
+#ifdef PVVOTE_ABLATE_U1_COMPUTE
+        float m = 3e38f;
+        for (int j = 0; j < kBytePix; ++j) nz[j] = rec.x + (float)j;
+#else
+        const float m = zrow(rec, nz);
+#endif
+        const uint64_t hit = __builtin_amdgcn_ballot_w64(m <= rec.z);   // flagged rows: rec.z = inf
+        uint32_t lo = pack4(nz[0], nz[1], nz[2], nz[3]), hi = pack4(nz[4], nz[5], nz[6], nz[7]);
+        bool skip = false;
+        if (hit) {
+            dmask |= 1ull << i;
+            if ((flagged >> i) & 1) {
+                skip = MODE != PV_VOTE_DENSE;
+            } else {
+                uint32_t bm = 0;
+#pragma unroll
+                for (int j = 0; j < kBytePix; ++j) bm |= (fabsf(nz[j]) <= rec.z ? 1u : 0u) << j;
+                int io = i;
+                asm volatile("" : "+s"(io));   // address math here, not an induction variable of the hot loop
+                band8[io * kWave + lane] = (uint8_t)bm;
+                if (MODE != PV_VOTE_DENSE) {
+                    lo &= ~((bm & 1u) | (bm & 2u) << 7 | (bm & 4u) << 14 | (bm & 8u) << 21);
+                    hi &= ~((bm >> 4 & 1u) | (bm >> 4 & 2u) << 7 | (bm >> 4 & 4u) << 14 | (bm >> 4 & 8u) << 21);
+                }
+            }
+        }
+        // (the row offset is made opaque so that the address stays a scalar
+        // base + 32-bit lane offset instead of a strength-reduced 64-bit VGPR pointer)
+        using gbyte = __attribute__((address_space(1))) uint8_t;
+        gbyte *rowp = (gbyte *)(a.out + (obase + rstep * i));
+        asm volatile("" : "+s"(rowp), "+v"(lof));
+#ifdef PVVOTE_ABLATE_U1_STORE
+        if (lo == 0x12345678u && hi == 0x9abcdef0u) skip = false; else skip = true;
+#endif
+        if (!skip) store((uint8_t *)(rowp + lof), lo, hi, partial);
+    };
+    auto rows = [&](auto partial) {
+        F4 ra = recs[0];
+        int i = 0;
+        for (; i + 1 < nh; i += 2) {
+            const F4 rb = recs[i + 1];
+            if ((i & 7) == 0) prio_by_remaining(rem_after + (uint32_t)(nh - i), wave_total);
+            row(ra, i, partial);
+            ra = recs[min(i + 2, kByteHB - 1)];
+            row(rb, i + 1, partial);
+        }
+        if (i < nh) row(ra, i, partial);
     };
     if (__builtin_amdgcn_ballot_w64(vmask != 0xffu)) rows(std::true_type{});
     else rows(std::false_type{});
 
-    // Exact pass over the deferred rows.
+    // Band rows: their pairs go to k_fix_bytes' queue (outside the hot loop:
+    // the queue's masks and atomics would crowd its registers).
+    {
+        uint64_t m = dmask & ~flagged;
+        while (m) {
+            const int i = __builtin_ctzll(m);
+            m &= m - 1;
+            if (enqueue(band8[i * kWave + lane], i)) dmask &= ~(1ull << i);
+        }
+    }
+    // Exact pass over what is left -- flagged rows, and band rows that found
+    // the queue full: the lane's pixels' reference operands are loaded once
+    // (one memory round trip), then the reference's sequence decides.
     if (a.dbg == 3) dmask = 0;   // profiling ablation only
-    while (dmask) {
-        const int i = __builtin_ctzll(dmask);
-        dmask &= dmask - 1;
-        const F4 r = recs[i];
-        uint32_t lo = 0, hi = 0;
-        if (__builtin_amdgcn_readfirstlane(__float_as_uint(r.w))) {
-            // row outside the fast domain: every pair exact
-#pragma unroll 1
-            for (int j = 0; j < kBytePix; ++j) {
-                const uint32_t bit = ((vmask >> j & 1) && exact_at(j, h0 + 8 * i)) ? 1u : 0u;
-                if (j < 4) lo |= bit << (8 * j);
-                else hi |= bit << (8 * (j - 4));
-            }
-        } else {
-            float z[kBytePix];
-            zrow(r, z);
-            lo = pack4(z[0], z[1], z[2], z[3]);
-            hi = pack4(z[4], z[5], z[6], z[7]);
-#pragma unroll 1
-            for (int j = 0; j < kBytePix; ++j) {
-                float zj = z[0];
+    if (dmask) {
+        float2 ec[kBytePix], ed[kBytePix];
 #pragma unroll
-                for (int k = 1; k < kBytePix; ++k) zj = j == k ? z[k] : zj;
-                const bool u = (vmask >> j & 1) && fabsf(zj) <= r.z;
-                if (__builtin_amdgcn_ballot_w64(u)) {
-                    if (u) {
-                        const uint32_t bit = 1u << (8 * (j & 3));
-                        const bool e = exact_at(j, h0 + 8 * i);
-                        if (j < 4) lo = e ? (lo | bit) : (lo & ~bit);
-                        else hi = e ? (hi | bit) : (hi & ~bit);
+        for (int j = 0; j < kBytePix; ++j) {
+            const int t = tb + j;
+            ec[j] = ed[j] = make_float2(0.f, 0.f);
+            if (vmask >> j & 1) {
+                ec[j] = *(const float2 *)(a.coords + (int64_t)t * 2);
+                ed[j] = *(const float2 *)(a.direct + ((int64_t)t * a.vn + v) * 2);
+            }
+        }
+        while (dmask) {
+            const int i = __builtin_ctzll(dmask);
+            dmask &= dmask - 1;
+            const int h = h0 + 8 * i;
+            const float2 q = *(const float2 *)(a.hypo + ((int64_t)h * a.vn + v) * 2);
+            uint8_t *p = a.out + (obase + rstep * i) + loff;
+            if ((flagged >> i) & 1) {
+                uint32_t lo = 0, hi = 0;
+#pragma unroll
+                for (int j = 0; j < kBytePix; ++j) {
+                    const uint32_t bit =
+                        ((vmask >> j & 1) && exact_vote(ed[j].x, ed[j].y, ec[j].x, ec[j].y, q.x, q.y, a.thr)) ? 1u : 0u;
+                    if (j < 4) lo |= bit << (8 * j);
+                    else hi |= bit << (8 * (j - 4));
+                }
+                store(p, lo, hi, std::true_type{});
+            } else {
+                const uint32_t bm = band8[i * kWave + lane];
+#pragma unroll
+                for (int j = 0; j < kBytePix; ++j) {
+                    if (bm >> j & 1) {
+                        const bool e = exact_vote(ed[j].x, ed[j].y, ec[j].x, ec[j].y, q.x, q.y, a.thr);
+                        if (MODE == PV_VOTE_DENSE) p[j] = e ? 1 : 0;
+                        else if (e) p[j] = 1;
                     }
                 }
             }
         }
-        store(orow + rstep * i, lo, hi);
+    }
+}
+
+// A wave's queued band pairs, decided by the reference's sequence at its
+// end: lane = entry, the three operand loads of up to 64 pairs in flight at
+// once; the byte goes over the wave's own earlier fast guess (dense, program
+// order) or is set (OR).
+template <int MODE>
+__device__ __forceinline__ void fix_queued(const ByteArgs &a, const uint2 *wq, uint32_t qn) {
+    for (uint32_t k = lane_id(); k < qn; k += kWave) {
+        const uint2 e = wq[k];
+        const uint32_t r = e.x, t = e.y;
+        const uint32_t v = r % (uint32_t)a.vn;
+        const float2 q = *(const float2 *)(a.hypo + (int64_t)r * 2);
+        const float2 c = *(const float2 *)(a.coords + (int64_t)t * 2);
+        const float2 d = *(const float2 *)(a.direct + ((int64_t)t * a.vn + v) * 2);
+        const bool in = exact_vote(d.x, d.y, c.x, c.y, q.x, q.y, a.thr);
+        uint8_t *o = a.out + (int64_t)r * a.tn + t;
+        if (MODE == PV_VOTE_DENSE) *o = in ? 1 : 0;
+        else if (in) *o = 1;
     }
 }
 
@@ -1819,13 +1934,24 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, int 
 template <int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_vote_bytes(ByteArgs a) {
     __shared__ F4 recs_all[4][kByteHB];
+    __shared__ uint8_t band_all[4][kByteHB * kWave];      // per deferred row: each lane's band-pair mask
+    __shared__ uint2 queue_all[4][kQueuePerWave];          // per wave: queued band pairs (row, pixel)
     F4 *recs = recs_all[threadIdx.x / 64];
+    uint8_t *band8 = band_all[threadIdx.x / 64];
     const int wave = uniform((int)(blockIdx.x * 4 + threadIdx.x / 64));
     const int64_t nwaves = (int64_t)gridDim.x * 4;
+#ifdef PVVOTE_TRACE_U1
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    uint64_t t_first = 0;
+    int nseg = 0, nrow = 0;
+#endif
     // 32-bit index math: rows = vn * nwin * hn < 2^31 (host-checked)
     const uint32_t per_v = (uint32_t)a.nwin * a.hn;        // sum over c of nwin * class_rows(c)
     uint32_t lo, hi;
     even_share(per_v * a.vn, (uint32_t)nwaves, (uint32_t)wave, &lo, &hi);
+    const uint32_t wave_total = hi - lo;
+    uint2 *wq = queue_all[threadIdx.x / 64];
+    uint32_t qn = 0;
     while (lo < hi) {
         const int v = (int)(lo / per_v);
         uint32_t r = lo - (uint32_t)v * per_v;
@@ -1836,9 +1962,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         const int i0 = (int)(r - (uint32_t)w * nc);
         const int i1 = min(nc, (int)min((uint32_t)(i0 + kByteHB), i0 + (hi - lo)));
         if (kByteWin * w - (int)((((int64_t)c * a.vn + v) * a.tn) & 7) < a.tn)   // window inside the row
-            vote_bytes_seg<MODE>(a, recs, uniform(v), uniform(c), uniform(w), uniform(i0), uniform(i1));
+            vote_bytes_seg<MODE>(a, recs, band8, uniform(v), uniform(c), uniform(w), uniform(i0), uniform(i1),
+                                 (hi - lo) - (uint32_t)(i1 - i0), wave_total, wq, qn);
         lo += i1 - i0;
+#ifdef PVVOTE_TRACE_U1
+        if (nseg == 0) t_first = __builtin_amdgcn_s_memrealtime();
+        ++nseg;
+        nrow += i1 - i0;
+#endif
     }
+    __builtin_amdgcn_wave_barrier();
+    fix_queued<MODE>(a, wq, qn);
+#ifdef PVVOTE_TRACE_U1
+    if (g_btrace && lane_id() == 0) {
+        uint32_t hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        g_btrace[wave * 4] = t_start;
+        g_btrace[wave * 4 + 1] = t_first;
+        g_btrace[wave * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+        g_btrace[wave * 4 + 3] = ((uint64_t)hw << 32) | ((uint64_t)nseg << 16) | (uint32_t)nrow;
+    }
+#endif
 }
 
 // KU:170-229
@@ -2086,6 +2230,20 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
 
 }  // namespace
 
+namespace {
+// workspace of pv_voting_for_hypothesis_ws: the prepass layouts
+struct BytesWs {
+    size_t prep, hypc, total;
+};
+BytesWs bytes_ws(int64_t tn, int64_t vn, int64_t hn) {
+    BytesWs w{};
+    w.prep = 0;
+    w.hypc = align_up((int64_t)sizeof(float4) * vn * tn, 256);
+    w.total = w.hypc + align_up((int64_t)sizeof(float2) * vn * hn, 256);
+    return w;
+}
+}  // namespace
+
 // ==========================================================================
 // C ABI
 // ==========================================================================
@@ -2127,27 +2285,34 @@ int pv_generate_hypothesis(const float *direct, const float *coords, const int32
     return last();
 }
 
-int pv_voting_for_hypothesis(const float *direct, const float *coords, const float *hypo, uint8_t *inliers,
-                             int32_t tn, int32_t vn, int32_t hn, float inlier_thresh, int32_t mode,
-                             pv_stream_t stream) {
+
+size_t pv_voting_for_hypothesis_workspace_size(int32_t tn, int32_t vn, int32_t hn) {
+    return (tn <= 0 || vn <= 0 || hn <= 0) ? 0 : bytes_ws(tn, vn, hn).total;
+}
+
+int pv_voting_for_hypothesis_ws(const float *direct, const float *coords, const float *hypo, uint8_t *inliers,
+                                int32_t tn, int32_t vn, int32_t hn, float inlier_thresh, int32_t mode,
+                                void *workspace, size_t workspace_bytes, pv_stream_t stream) {
     if (!direct || !coords || !hypo || !inliers || tn < 0 || vn <= 0 || hn < 0) return PV_EINVAL;
     if (mode != PV_VOTE_OR && mode != PV_VOTE_DENSE) return PV_EINVAL;
     if (tn == 0 || hn == 0) return PV_OK;
+    const BytesWs L = bytes_ws(tn, vn, hn);
+    if (!workspace || workspace_bytes < L.total) return PV_EINVAL;
     VoteArgs fc{};
     fast_constants(inlier_thresh, &fc);
     hipStream_t s = (hipStream_t)stream;
-    // stream-ordered scratch for the prepass layouts: safe for concurrent streams and graph capture
-    const size_t prep_bytes = sizeof(float4) * (size_t)vn * tn, hyp_bytes = sizeof(float2) * (size_t)vn * hn;
-    char *scratch = nullptr;
-    hipError_t e = hipMallocAsync((void **)&scratch, prep_bytes + hyp_bytes, s);
-    if (e != hipSuccess) return rc(e);
-    ByteArgs ba{(const float4 *)scratch, (const float2 *)(scratch + prep_bytes), direct, coords, hypo, inliers,
-                tn, vn, hn, 0, fc.fast, fc.thr, fc.tau, fc.gzf, fc.gzr};
+    char *ws = (char *)workspace;
+    ByteArgs ba{};
+    ba.prep = (const float4 *)(ws + L.prep);
+    ba.hypc = (const float2 *)(ws + L.hypc);
+    ba.direct = direct; ba.coords = coords; ba.hypo = hypo; ba.out = inliers;
+    ba.tn = tn; ba.vn = vn; ba.hn = hn;
+    ba.fast = fc.fast; ba.thr = fc.thr; ba.tau = fc.tau; ba.gzf = fc.gzf; ba.gzr = fc.gzr;
     ba.nwin = (tn + 7 + kByteWin - 1) / kByteWin;
     if (const char *e3 = getenv("PVVOTE_DEBUG_BYTES")) ba.dbg = atoi(e3);
     const int64_t nprep = (int64_t)vn * tn + (int64_t)vn * hn;
-    k_prep_api<<<(unsigned)((nprep + 255) / 256), 256, 0, s>>>(direct, coords, hypo, (float4 *)scratch,
-                                                                (float2 *)(scratch + prep_bytes), tn, vn, hn);
+    k_prep_api<<<(unsigned)((nprep + 255) / 256), 256, 0, s>>>(direct, coords, hypo, (float4 *)(ws + L.prep),
+                                                                (float2 *)(ws + L.hypc), tn, vn, hn);
     // persistent grid: every block resident, >= ~rpw rows per wave
     const int64_t rows = (int64_t)vn * ba.nwin * hn;
     if (rows >= (1ll << 31)) return PV_EINVAL;   // the kernel's 32-bit row index (a >2 TB mask)
@@ -2157,7 +2322,23 @@ int pv_voting_for_hypothesis(const float *direct, const float *coords, const flo
         k_vote_bytes<PV_VOTE_DENSE><<<vote_grid_steps(rows * 128 / rpw, (const void *)k_vote_bytes<PV_VOTE_DENSE>), 256, 0, s>>>(ba);
     else
         k_vote_bytes<PV_VOTE_OR><<<vote_grid_steps(rows * 128 / rpw, (const void *)k_vote_bytes<PV_VOTE_OR>), 256, 0, s>>>(ba);
-    int r = last();
+    return last();
+}
+
+int pv_voting_for_hypothesis(const float *direct, const float *coords, const float *hypo, uint8_t *inliers,
+                             int32_t tn, int32_t vn, int32_t hn, float inlier_thresh, int32_t mode,
+                             pv_stream_t stream) {
+    if (!direct || !coords || !hypo || !inliers || tn < 0 || vn <= 0 || hn < 0) return PV_EINVAL;
+    if (mode != PV_VOTE_OR && mode != PV_VOTE_DENSE) return PV_EINVAL;
+    if (tn == 0 || hn == 0) return PV_OK;
+    hipStream_t s = (hipStream_t)stream;
+    // stream-ordered scratch: safe for concurrent streams and graph capture
+    const size_t bytes = pv_voting_for_hypothesis_workspace_size(tn, vn, hn);
+    void *scratch = nullptr;
+    hipError_t e = hipMallocAsync(&scratch, bytes, s);
+    if (e != hipSuccess) return rc(e);
+    int r = pv_voting_for_hypothesis_ws(direct, coords, hypo, inliers, tn, vn, hn, inlier_thresh, mode, scratch,
+                                        bytes, stream);
     e = hipFreeAsync(scratch, s);
     return r ? r : rc(e);
 }
@@ -2206,6 +2387,9 @@ int pv_vote_counts(const float *direct, const float *coords, const float *hypo, 
 
 // debug only (not in pvvote.h): per-wave timestamps of the next pipeline vote launches
 void pv_debug_set_vote_trace(uint64_t *buf) { g_vote_trace = buf; }
+#ifdef PVVOTE_TRACE_U1
+int pv_debug_set_bytes_trace(uint64_t *buf) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_btrace), &buf, sizeof(buf)); }
+#endif
 int pv_debug_compact_trace(int on, uint64_t *host, int n) {
     if (host) return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ctrace), sizeof(uint64_t) * (size_t)n);
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_ctrace_on), &on, sizeof(int));

@@ -107,6 +107,31 @@ def test_guard_band_stress(seed, device, rv):
         np.testing.assert_array_equal(cnt, ref.sum(2), err_msg=f"thr={thr}")
 
 
+@pytest.mark.parametrize("full_queue", [False, True])
+def test_band_pairs_both_modes(full_queue, device, rv, monkeypatch):
+    """Band pairs go through k_fix_bytes' queue (or, with the queue full, the
+    in-kernel exact pass): dense and OR modes, thresholds on reference cosines."""
+    if full_queue:
+        monkeypatch.setenv("PVVOTE_DEBUG_BYTES", "4")
+    rng = np.random.default_rng(7)
+    tn, vn, hn = 2500, 2, 96
+    coords = np.stack([rng.integers(0, 640, tn), rng.integers(0, 480, tn)], 1).astype(np.float32)
+    ang = rng.uniform(-np.pi, np.pi, (tn, vn))
+    direct = np.stack([np.cos(ang), np.sin(ang)], -1).astype(np.float32)
+    hyp = np.stack([rng.uniform(-50, 690, (hn, vn)), rng.uniform(-50, 530, (hn, vn))], -1).astype(np.float32)
+    hyp[5:9] = coords[rng.integers(0, tn, (4, vn))]
+    d = hyp[20, 0] - coords[11]
+    thr = float(np.float32(np.dot(d, direct[11, 0]) / (np.linalg.norm(d) * np.linalg.norm(direct[11, 0]))))
+    init = (rng.random((hn, vn, tn)) < 0.2).astype(np.uint8) * 3
+    for dense in (True, False):
+        ref = np.zeros((hn, vn, tn), np.uint8) if dense else init.copy()
+        O.voting_for_hypothesis(direct, coords, hyp, ref, thr)
+        out = torch.zeros(ref.shape, dtype=torch.uint8, device=device) if dense else cu(init, device)
+        fn = rv.voting_for_hypothesis_dense if dense else rv.voting_for_hypothesis
+        fn(cu(direct, device), cu(coords, device), cu(hyp, device), out, thr)
+        np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"dense={dense}")
+
+
 def test_vp_kernels(device, rv):
     g = G.load("vp_kernels")
     hyp = rv.generate_hypothesis_vanishing_point(cu(g["direct"], device), cu(g["coords"], device),

@@ -1,7 +1,8 @@
-"""Debug: phase stamps (s_memrealtime, 100 MHz) of the byte-output vote
-kernel's first item per wave: 0 entry, 1 pixels loaded, 2 reductions, 3
-records, 4 wave end.  GPU only."""
+"""Debug: per-wave phase stamps of k_vote_bytes (voting_for_hypothesis, dense)
+from a library built with -DPVVOTE_TRACE_U1 (variants/u1trace.so):
+start, end of the first segment, end; s_memrealtime at 100 MHz.  GPU only."""
 import ctypes
+import os
 import sys
 
 import numpy as np
@@ -16,30 +17,29 @@ L.pv_debug_set_bytes_trace.argtypes = [ctypes.c_void_p]
 f = synth.synthetic_field(1234)
 m = np.argmax(f["seg"][0], 0) == 1
 rows, cols = np.nonzero(m)
-VN, hn = 9, 512
+VN, tn, hn = 9, 29861, int(os.environ.get("U1_HN", "512"))
 coords = torch.from_numpy(np.stack([cols, rows], 1).astype(np.float32)).cuda()
 direct = torch.from_numpy(np.ascontiguousarray(
     f["vertex"][0].reshape(VN, 2, 480, 640)[:, :, rows, cols].transpose(2, 0, 1))).cuda()
-tn = coords.shape[0]
 idxs = torch.randint(0, tn, (hn, VN, 2), dtype=torch.int32, device="cuda")
 hyp = rv.generate_hypothesis(direct, coords, idxs)
 inl = torch.empty((hn, VN, tn), dtype=torch.uint8, device="cuda")
-buf = torch.zeros(8 * 16384, dtype=torch.int64, device="cuda")
-for it in range(3):
+buf = torch.zeros(65536 * 4, dtype=torch.int64, device="cuda")
+for it in range(4):
     buf.zero_()
-    L.pv_debug_set_bytes_trace(ctypes.c_void_p(buf.data_ptr()) if it == 2 else None)
+    L.pv_debug_set_bytes_trace(ctypes.c_void_p(buf.data_ptr() if it == 3 else 0))
     rv.voting_for_hypothesis_dense(direct, coords, hyp, inl, 0.99)
     torch.cuda.synchronize()
-t = buf.view(-1, 8).cpu().numpy()[:, :5]
+t = buf.view(-1, 4).cpu().numpy()
 t = t[t[:, 0] > 0]
-t0 = t[:, 0].min()
-us = (t - t0) / 100.0
-print("waves", len(t))
-names = ["entry", "loaded", "reduced", "records", "end"]
-for k in range(5):
-    q = np.percentile(us[:, k], [0, 10, 50, 90, 100])
-    print(f"{names[k]:8s}", " ".join(f"{v:7.2f}" for v in q))
-for k in range(1, 5):
-    d = us[:, k] - us[:, k - 1]
-    q = np.percentile(d, [0, 10, 50, 90, 100])
-    print(f"d{names[k]:7s}", " ".join(f"{v:7.2f}" for v in q))
+s, f1, e = t[:, 0], t[:, 1], t[:, 2]
+nrow, nseg = t[:, 3] & 0xffff, (t[:, 3] >> 16) & 0xffff
+t0 = s.min()
+print("waves", len(t), "span us", (e.max() - t0) / 100.0, "rows/wave median", np.median(nrow), "segs", np.bincount(nseg))
+for name, x in (("start", (s - t0) / 100), ("first", (f1 - s) / 100), ("end", (e - t0) / 100), ("life", (e - s) / 100)):
+    q = np.percentile(x, [0, 1, 10, 50, 90, 99, 100])
+    print(f"{name:6s}", " ".join(f"{v:7.2f}" for v in q))
+hist, edges = np.histogram((e - t0) / 100, bins=20)
+print("end histogram:", list(zip(np.round(edges[:-1], 1).tolist(), hist.tolist())))
+hist, edges = np.histogram((s - t0) / 100, bins=20)
+print("start histogram:", list(zip(np.round(edges[:-1], 1).tolist(), hist.tolist())))

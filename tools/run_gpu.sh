@@ -27,6 +27,10 @@ for s in "$@"; do
     pmchbm) step pmchbm1 600 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d "$PWD/gpurun_out/pmc_fetch" -o bench -- python3 bench.py --skip-cpu --skip-e2e --steps 20 &&
             step pmchbm2 600 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d "$PWD/gpurun_out/pmc_write" -o bench -- python3 bench.py --skip-cpu --skip-e2e --steps 20 ;;
     pmcvalu) step pmcvalu 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -T --output-format csv -d "$PWD/gpurun_out/pmc_valu" -o bench -- python3 bench.py --skip-cpu --skip-e2e --steps 20 ;;
+    pmcu1v) for v in u1base u1nostore; do PVVOTE_LIB=variants/$v.so step pmcu1_$v 300 rocprofv3 --kernel-include-regex k_vote_bytes --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE -T --output-format csv -d "$PWD/gpurun_out/pmcu1_$v" -o v -- python3 tools/u1_probe.py; done ;;
+    profu1v) for v in u1base u1nostore u1nocomp; do PVVOTE_LIB=variants/$v.so step profu1_$v 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$PWD/gpurun_out/profu1_$v" -o u1 -- python3 tools/u1_probe.py; done ;;
+    profu1x) PVVOTE_DEBUG_BYTES=3 step profu1x 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$PWD/gpurun_out/profu1x" -o u1 -- python3 tools/u1_probe.py ;;
+    profu1) step profu1 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$PWD/gpurun_out/profu1" -o u1 -- python3 tools/u1_probe.py ;;
     listpmc) step listpmc 300 rocprofv3 -L ;;
     pmcvote) step pmcvote1 600 rocprofv3 --kernel-include-regex k_vote_count --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_INST_CYCLES_SALU -T --output-format csv -d "$PWD/gpurun_out/pmc_vote1" -o v -- python3 bench.py --skip-cpu --skip-e2e --skip-u1 --steps 10 &&
              step pmcvote2 600 rocprofv3 --kernel-include-regex k_vote_count --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_WAVES SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE SQ_INSTS_VALU_TRANS_F32 -T --output-format csv -d "$PWD/gpurun_out/pmc_vote2" -o v -- python3 bench.py --skip-cpu --skip-e2e --skip-u1 --steps 10 &&
