@@ -1541,19 +1541,18 @@ __global__ __launch_bounds__(256) void k_generate_api(const float *direct, const
 // bytes).  Mode OR writes only the inlier bytes (reference semantics: the
 // caller's buffer keeps its other bytes), DENSE writes every byte.
 //
-// Rows (h, v) start at arbitrary byte offsets R = (h*vn + v)*tn, but rows of
-// hypotheses h = c (mod 8) share s = R mod 8.  A wave takes rows of one
-// keypoint v and one class c inside one 512-byte window w: lane l owns the
-// 8-byte aligned word at R - s + 512w + 8l -- pixels t = 512w - s + 8l + j,
-// j < 8 -- and writes it with one 8-byte store per row.  The work is the
-// linearised (v, c, w, row) space cut into equal ranges, one per wave, rows
-// fastest, so a wave prepares its pixels once per (c, w) segment.  A prepass
-// (k_prep_api) lays the operands out for contiguous reads: pixels keypoint-
-// major as (ux, uy, cx, cy), hypotheses keypoint- and class-major.  The vote
-// test is vote_segment's rotated-frame test (5 FMAs per pair); the inlier
-// bytes are the sign bytes of z gathered with v_perm.  Pairs inside the
-// guard band, and hypotheses / pixels outside the fast domain, take the
-// reference's exact sequence.
+// A wave takes one item: keypoint v, a window of 512 pixels w and 64
+// consecutive hypotheses; lane l owns pixels t = 512w + 8l + j, j < 8, and
+// writes their 8 bytes of each row (h, v) at R = (h*vn + v)*tn + t with one
+// 8-byte store, unaligned as the rows are (measured as fast as aligned
+// stores on gfx950).  One item per wave, every item's operand loads at the
+// start of the launch, before the store stream fills the memory system.  A
+// prepass (k_prep_api) lays the pixels out keypoint-major as (ux, uy, cx,
+// cy).  The vote test is vote_segment's rotated-frame test (5 FMAs per
+// pair); the inlier bytes are the signs of -z gathered with v_perm.  Pairs
+// inside the guard band go to a per-wave LDS queue decided by the
+// reference's sequence at the wave's end; hypotheses / pixels outside the
+// fast domain take it for their whole row.
 constexpr int kBytePix = 8;
 constexpr int kByteWin = kWave * kBytePix;      // bytes of a row per segment
 constexpr int kByteHB = 64;                      // hypothesis records per batch
@@ -1565,29 +1564,21 @@ __device__ uint64_t *g_btrace;      // debug build only: per-wave phase stamps o
 
 struct ByteArgs {
     const float4 *prep;    // [vn][tn] (ux, uy, cx, cy), see k_prep_api
-    const float2 *hypc;    // [vn][hn] class-major: hypothesis c + 8i at [v][cbase(c) + i]
     const float *direct;   // [tn][vn][2]
     const float *coords;   // [tn][2]
     const float *hypo;     // [hn][vn][2]
     uint8_t *out;          // [hn][vn][tn]
-    int tn, vn, hn, nwin, fast;
+    int tn, vn, hn, nwin, nhg, fast;
     float thr, tau, gzf, gzr;
     int dbg;               // profiling ablation (PVVOTE_DEBUG_BYTES), 0 = normal
 };
 
-__host__ __device__ inline int class_rows(int hn, int c) { return c < hn ? (hn - c + 7) / 8 : 0; }
-__host__ __device__ inline int class_base(int hn, int c) {   // rows of classes < c
-    int b = 0;
-    for (int k = 0; k < c; ++k) b += class_rows(hn, k);
-    return b;
-}
-
 // Operand layouts of the byte-output kernel.  Pixel (t, v): (ux, uy, cx, cy)
 // with u the direction rounded per component; (0, 0) for a pixel that never
 // votes (norm1 < 1e-6 or NaN, KU:119-121, or non-finite coordinates) and
-// ux = NaN for one outside the fast domain.  Hypotheses regrouped by class.
-__global__ __launch_bounds__(256) void k_prep_api(const float *direct, const float *coords, const float *hypo,
-                                                  float4 *prep, float2 *hypc, int tn, int vn, int hn) {
+// ux = NaN for one outside the fast domain.
+__global__ __launch_bounds__(256) void k_prep_api(const float *direct, const float *coords, float4 *prep, int tn,
+                                                  int vn) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t np = (int64_t)vn * tn;
     if (i < np) {
@@ -1602,15 +1593,9 @@ __global__ __launch_bounds__(256) void k_prep_api(const float *direct, const flo
             q = (n1 <= kN1Max) ? make_float4(d.x * rs, d.y * rs, c.x, c.y)
                                : make_float4(__builtin_nanf(""), 0.f, c.x, c.y);
         prep[i] = q;
-    } else if (i < np + (int64_t)vn * hn) {
-        const int64_t k = i - np;
-        const int v = (int)(k / hn), h = (int)(k - (int64_t)v * hn);
-        const int c = h & 7;
-        hypc[(int64_t)v * hn + class_base(hn, c) + (h >> 3)] = *(const float2 *)(hypo + ((int64_t)h * vn + v) * 2);
     }
 }
 
-// rows [i0, i1) (i1 - i0 <= kByteHB) of keypoint v, class c, window w
 // Issue priority from the rows a wave still has (0..3), as in vote_segment:
 // otherwise the SIMD favours its oldest wave, equal shares finish staggered
 // and the last waves of each SIMD run alone at a fraction of the issue rate.
@@ -1622,26 +1607,23 @@ __device__ __forceinline__ void prio_by_remaining(uint32_t remaining, uint32_t t
     else __builtin_amdgcn_s_setprio(0);
 }
 
+// rows h0 + i, i < nh (<= kByteHB), of keypoint v, pixels of window w
 template <int MODE>
-__device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint8_t *band8, int v, int c, int w,
-                                               int i0, int i1, uint32_t rem_after, uint32_t wave_total,
-                                               uint2 *wq, uint32_t &qn) {
+__device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint8_t *band8, int v, int w, int h0,
+                                               int nh, uint32_t rem_after, uint32_t wave_total, uint2 *wq,
+                                               uint32_t &qn, uint64_t *tsetup, const float4 *stage) {
     const uint32_t qcap = a.dbg == 4 ? 1u : kQueuePerWave;   // (dbg 4: test hook, a full queue)
     const int lane = lane_id();
     const float ntau = -a.tau;
-    const int nh = i1 - i0;
-    const int h0 = c + 8 * i0;                                  // rows h0 + 8i, i < nh
-    const int64_t R0 = ((int64_t)h0 * a.vn + v) * a.tn;
-    const int s = (int)(R0 & 7);
-    const int tb = kByteWin * w - s + kBytePix * lane;          // lane's first pixel
-    const int64_t rstep = (int64_t)8 * a.vn * a.tn;             // R(h + 8) - R(h)
-    // row i's word of this lane: wave-uniform offset (SGPRs) + 32-bit lane offset
-    const int64_t obase = R0 - s + (int64_t)kByteWin * w;
+    const int tb = kByteWin * w + kBytePix * lane;              // lane's first pixel
+    const int64_t rstep = (int64_t)a.vn * a.tn;                 // R(h + 1) - R(h)
+    // row i's bytes of this lane: wave-uniform offset (SGPRs) + 32-bit lane offset
+    const int64_t obase = ((int64_t)h0 * a.vn + v) * a.tn + (int64_t)kByteWin * w;
     const uint32_t loff = kBytePix * lane;
 
     // ---- operands: all loads issued together ----
     float2 hq = make_float2(0.f, 0.f);
-    if (lane < nh) hq = a.hypc[(int64_t)v * a.hn + class_base(a.hn, c) + i0 + lane];
+    if (lane < nh) hq = *(const float2 *)(a.hypo + ((int64_t)(h0 + lane) * a.vn + v) * 2);
     uint32_t vmask = 0, okmask = 0;
     bool exo = false;
     float fu[kBytePix], fv[kBytePix], fk1[kBytePix], fk2[kBytePix];   // (ux, uy, cx, cy) first
@@ -1651,11 +1633,12 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint
         const int t = tb + j;
         fu[j] = fv[j] = fk1[j] = fk2[j] = 0.f;
         if (t >= 0 && t < a.tn) {
-            const float4 q = pp[t];
+            const float4 q = stage ? stage[kBytePix * lane + j] : pp[t];   // (block-staged window, or global)
             fu[j] = q.x; fv[j] = q.y; fk1[j] = q.z; fk2[j] = q.w;
             vmask |= 1u << j;
         }
     }
+    if (stage) __syncthreads();   // the staging area is the block's band masks from here on
 #pragma unroll
     for (int j = 0; j < kBytePix; ++j) {
         exo |= fu[j] != fu[j];                                  // outside the fast domain
@@ -1724,23 +1707,42 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint
         __builtin_amdgcn_wave_barrier();
     }
 
+    typedef uint64_t u64a1 __attribute__((aligned(1)));   // rows start at any byte
     auto store = [&](uint8_t *p, uint32_t lo, uint32_t hi, auto partial) {
         if (!decltype(partial)::value || vmask == 0xffu) {
+            const uint64_t x = (uint64_t)hi << 32 | lo;
             if (MODE == PV_VOTE_DENSE) {
-                *(uint2 *)p = make_uint2(lo, hi);
+                *(u64a1 *)p = x;
             } else {
                 // KU:125 sets inlier bytes to 1 and leaves the others
-                const uint2 old = *(const uint2 *)p;
-                *(uint2 *)p = make_uint2((old.x & ~(lo * 0xffu)) | lo, (old.y & ~(hi * 0xffu)) | hi);
+                const uint64_t old = *(const u64a1 *)p;
+                *(u64a1 *)p = (old & ~(x * 0xffu)) | x;
             }
-        } else {
-#pragma unroll
-            for (int j = 0; j < kBytePix; ++j) {
-                if (vmask >> j & 1) {
-                    const uint8_t bit = (uint8_t)(((j < 4 ? lo : hi) >> (8 * (j & 3))) & 1u);
-                    if (MODE == PV_VOTE_DENSE) p[j] = bit;
-                    else if (bit) p[j] = 1;
-                }
+        } else if (vmask) {
+            // a row's last pixels (vmask is a prefix): 4 + 2 + 1 bytes at most
+            typedef uint32_t u32a1 __attribute__((aligned(1)));
+            typedef uint16_t u16a1 __attribute__((aligned(1)));
+            const int n = __builtin_popcount(vmask);
+            uint64_t x = (uint64_t)hi << 32 | lo;
+            int o = 0;
+            if (n & 4) {
+                const uint32_t y = (uint32_t)x;
+                if (MODE == PV_VOTE_DENSE) *(u32a1 *)(p + o) = y;
+                else *(u32a1 *)(p + o) = (*(const u32a1 *)(p + o) & ~(y * 0xffu)) | y;
+                x >>= 32;
+                o += 4;
+            }
+            if (n & 2) {
+                const uint16_t y = (uint16_t)x;
+                if (MODE == PV_VOTE_DENSE) *(u16a1 *)(p + o) = y;
+                else *(u16a1 *)(p + o) = (uint16_t)((*(const u16a1 *)(p + o) & ~(y * 0xffu)) | y);
+                x >>= 16;
+                o += 2;
+            }
+            if (n & 1) {
+                const uint8_t y = (uint8_t)x;
+                if (MODE == PV_VOTE_DENSE) p[o] = y;
+                else if (y) p[o] = 1;
             }
         }
     };
@@ -1766,6 +1768,7 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint
         return m;
     };
 
+    if (tsetup && *tsetup == 0) *tsetup = __builtin_amdgcn_s_memrealtime();   // (trace builds only)
     // Hot loop: the fast decision of every pair, one 8-byte store per row.
     // A row with a pair inside the band records which (an 8-bit mask per lane
     // in LDS) and its word is stored with those bytes as the fast guess
@@ -1788,7 +1791,7 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint
         }
         const uint32_t base = qn;
         qn = min(base + tot, qcap);
-        const uint32_t r = (uint32_t)((h0 + 8 * i) * a.vn + v);
+        const uint32_t r = (uint32_t)((h0 + i) * a.vn + v);
         uint32_t k = base + pre;
 #pragma unroll
         for (int j = 0; j < kBytePix; ++j) {
@@ -1882,7 +1885,7 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint
         while (dmask) {
             const int i = __builtin_ctzll(dmask);
             dmask &= dmask - 1;
-            const int h = h0 + 8 * i;
+            const int h = h0 + i;
             const float2 q = *(const float2 *)(a.hypo + ((int64_t)h * a.vn + v) * 2);
             uint8_t *p = a.out + (obase + rstep * i) + loff;
             if ((flagged >> i) & 1) {
@@ -1930,57 +1933,62 @@ __device__ __forceinline__ void fix_queued(const ByteArgs &a, const uint2 *wq, u
     }
 }
 
-// Balanced persistent waves over the linearised (v, c, window, row) space.
+// One item per wave: (keypoint v, window w, hypothesis group g of kByteHB),
+// g fastest; a wave beyond the items exits.
 template <int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_vote_bytes(ByteArgs a) {
     __shared__ F4 recs_all[4][kByteHB];
-    __shared__ uint8_t band_all[4][kByteHB * kWave];      // per deferred row: each lane's band-pair mask
+    __shared__ alignas(16) uint8_t band_all[4][kByteHB * kWave];   // per deferred row: each lane's band-pair mask
     __shared__ uint2 queue_all[4][kQueuePerWave];          // per wave: queued band pairs (row, pixel)
     F4 *recs = recs_all[threadIdx.x / 64];
     uint8_t *band8 = band_all[threadIdx.x / 64];
+    uint2 *wq = queue_all[threadIdx.x / 64];
     const int wave = uniform((int)(blockIdx.x * 4 + threadIdx.x / 64));
-    const int64_t nwaves = (int64_t)gridDim.x * 4;
 #ifdef PVVOTE_TRACE_U1
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    uint64_t t_first = 0;
-    int nseg = 0, nrow = 0;
+    uint64_t t_setup = 0;
+    uint64_t *tsetup = &t_setup;
+#else
+    uint64_t *tsetup = nullptr;
 #endif
-    // 32-bit index math: rows = vn * nwin * hn < 2^31 (host-checked)
-    const uint32_t per_v = (uint32_t)a.nwin * a.hn;        // sum over c of nwin * class_rows(c)
-    uint32_t lo, hi;
-    even_share(per_v * a.vn, (uint32_t)nwaves, (uint32_t)wave, &lo, &hi);
-    const uint32_t wave_total = hi - lo;
-    uint2 *wq = queue_all[threadIdx.x / 64];
-    uint32_t qn = 0;
-    while (lo < hi) {
-        const int v = (int)(lo / per_v);
-        uint32_t r = lo - (uint32_t)v * per_v;
-        int c = 0;
-        while (r >= (uint32_t)a.nwin * class_rows(a.hn, c)) { r -= (uint32_t)a.nwin * class_rows(a.hn, c); ++c; }
-        const int nc = class_rows(a.hn, c);
-        const int w = (int)(r / (uint32_t)nc);
-        const int i0 = (int)(r - (uint32_t)w * nc);
-        const int i1 = min(nc, (int)min((uint32_t)(i0 + kByteHB), i0 + (hi - lo)));
-        if (kByteWin * w - (int)((((int64_t)c * a.vn + v) * a.tn) & 7) < a.tn)   // window inside the row
-            vote_bytes_seg<MODE>(a, recs, band8, uniform(v), uniform(c), uniform(w), uniform(i0), uniform(i1),
-                                 (hi - lo) - (uint32_t)(i1 - i0), wave_total, wq, qn);
-        lo += i1 - i0;
-#ifdef PVVOTE_TRACE_U1
-        if (nseg == 0) t_first = __builtin_amdgcn_s_memrealtime();
-        ++nseg;
-        nrow += i1 - i0;
-#endif
+    const uint32_t nitems = (uint32_t)a.vn * a.nwin * a.nhg;   // < 2^31 (host-checked)
+    // With the hypothesis groups in fours (hn a multiple of 256) a block's
+    // four items share (v, w): the block stages the window's pixels in LDS
+    // once (the band-mask area, free until the hot loop) instead of four
+    // times from L2 -- every item loads at the launch's start at once.
+    const float4 *stage = nullptr;
+    if (a.nhg % 4 == 0) {
+        // (nitems is then a multiple of 4: every wave of every block has an item)
+        const uint32_t rest = (uint32_t)blockIdx.x * 4 / a.nhg;
+        const int w = (int)(rest % (uint32_t)a.nwin), v = (int)(rest / (uint32_t)a.nwin);
+        float4 *st = (float4 *)&band_all[0][0];
+        const float4 *pp = a.prep + (int64_t)v * a.tn;
+        for (int k = threadIdx.x; k < kByteWin; k += 256) {
+            const int t = kByteWin * w + k;
+            if (t < a.tn) st[k] = pp[t];
+        }
+        __syncthreads();
+        stage = st;
+    } else if ((uint32_t)wave >= nitems) {
+        return;
     }
+    const uint32_t g = (uint32_t)wave % a.nhg, rest = (uint32_t)wave / a.nhg;
+    const int w = (int)(rest % (uint32_t)a.nwin), v = (int)(rest / (uint32_t)a.nwin);
+    const int h0 = (int)g * kByteHB, nh = min(kByteHB, a.hn - h0);
+    uint32_t qn = 0;
+    vote_bytes_seg<MODE>(a, recs, band8, uniform(v), uniform(w), uniform(h0), uniform(nh), 0u, (uint32_t)nh, wq, qn,
+                         tsetup, stage);
+#ifdef PVVOTE_TRACE_U1
+    const uint64_t t_first = __builtin_amdgcn_s_memrealtime();
+#endif
     __builtin_amdgcn_wave_barrier();
     fix_queued<MODE>(a, wq, qn);
 #ifdef PVVOTE_TRACE_U1
     if (g_btrace && lane_id() == 0) {
-        uint32_t hw;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         g_btrace[wave * 4] = t_start;
         g_btrace[wave * 4 + 1] = t_first;
         g_btrace[wave * 4 + 2] = __builtin_amdgcn_s_memrealtime();
-        g_btrace[wave * 4 + 3] = ((uint64_t)hw << 32) | ((uint64_t)nseg << 16) | (uint32_t)nrow;
+        g_btrace[wave * 4 + 3] = t_setup;
     }
 #endif
 }
@@ -2231,15 +2239,15 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
 }  // namespace
 
 namespace {
-// workspace of pv_voting_for_hypothesis_ws: the prepass layouts
+// workspace of pv_voting_for_hypothesis_ws: the prepass layout
 struct BytesWs {
-    size_t prep, hypc, total;
+    size_t prep, total;
 };
 BytesWs bytes_ws(int64_t tn, int64_t vn, int64_t hn) {
+    (void)hn;
     BytesWs w{};
     w.prep = 0;
-    w.hypc = align_up((int64_t)sizeof(float4) * vn * tn, 256);
-    w.total = w.hypc + align_up((int64_t)sizeof(float2) * vn * hn, 256);
+    w.total = align_up((int64_t)sizeof(float4) * vn * tn, 256);
     return w;
 }
 }  // namespace
@@ -2304,24 +2312,21 @@ int pv_voting_for_hypothesis_ws(const float *direct, const float *coords, const 
     char *ws = (char *)workspace;
     ByteArgs ba{};
     ba.prep = (const float4 *)(ws + L.prep);
-    ba.hypc = (const float2 *)(ws + L.hypc);
     ba.direct = direct; ba.coords = coords; ba.hypo = hypo; ba.out = inliers;
     ba.tn = tn; ba.vn = vn; ba.hn = hn;
     ba.fast = fc.fast; ba.thr = fc.thr; ba.tau = fc.tau; ba.gzf = fc.gzf; ba.gzr = fc.gzr;
-    ba.nwin = (tn + 7 + kByteWin - 1) / kByteWin;
+    ba.nwin = (tn + kByteWin - 1) / kByteWin;
+    ba.nhg = (hn + kByteHB - 1) / kByteHB;
     if (const char *e3 = getenv("PVVOTE_DEBUG_BYTES")) ba.dbg = atoi(e3);
-    const int64_t nprep = (int64_t)vn * tn + (int64_t)vn * hn;
-    k_prep_api<<<(unsigned)((nprep + 255) / 256), 256, 0, s>>>(direct, coords, hypo, (float4 *)(ws + L.prep),
-                                                                (float2 *)(ws + L.hypc), tn, vn, hn);
-    // persistent grid: every block resident, >= ~rpw rows per wave
-    const int64_t rows = (int64_t)vn * ba.nwin * hn;
-    if (rows >= (1ll << 31)) return PV_EINVAL;   // the kernel's 32-bit row index (a >2 TB mask)
-    int64_t rpw = 16;
-    if (const char *e2 = getenv("PVVOTE_BYTES_RPW")) rpw = atoi(e2);   // experiment knob
+    const int64_t nprep = (int64_t)vn * tn;
+    k_prep_api<<<(unsigned)((nprep + 255) / 256), 256, 0, s>>>(direct, coords, (float4 *)(ws + L.prep), tn, vn);
+    const int64_t items = (int64_t)vn * ba.nwin * ba.nhg;
+    if (items >= (1ll << 31)) return PV_EINVAL;   // the kernel's 32-bit item index
+    const unsigned grid = (unsigned)((items + 3) / 4);
     if (mode == PV_VOTE_DENSE)
-        k_vote_bytes<PV_VOTE_DENSE><<<vote_grid_steps(rows * 128 / rpw, (const void *)k_vote_bytes<PV_VOTE_DENSE>), 256, 0, s>>>(ba);
+        k_vote_bytes<PV_VOTE_DENSE><<<grid, 256, 0, s>>>(ba);
     else
-        k_vote_bytes<PV_VOTE_OR><<<vote_grid_steps(rows * 128 / rpw, (const void *)k_vote_bytes<PV_VOTE_OR>), 256, 0, s>>>(ba);
+        k_vote_bytes<PV_VOTE_OR><<<grid, 256, 0, s>>>(ba);
     return last();
 }
 

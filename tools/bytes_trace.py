@@ -32,14 +32,22 @@ for it in range(4):
     torch.cuda.synchronize()
 t = buf.view(-1, 4).cpu().numpy()
 t = t[t[:, 0] > 0]
-s, f1, e = t[:, 0], t[:, 1], t[:, 2]
-nrow, nseg = t[:, 3] & 0xffff, (t[:, 3] >> 16) & 0xffff
+s, f1, e, su = t[:, 0], t[:, 1], t[:, 2], t[:, 3]
 t0 = s.min()
-print("waves", len(t), "span us", (e.max() - t0) / 100.0, "rows/wave median", np.median(nrow), "segs", np.bincount(nseg))
-for name, x in (("start", (s - t0) / 100), ("first", (f1 - s) / 100), ("end", (e - t0) / 100), ("life", (e - s) / 100)):
+print("waves", len(t), "span us", (e.max() - t0) / 100.0)
+for name, x in (("start", (s - t0) / 100), ("setup", (su - s) / 100), ("first", (f1 - s) / 100),
+                ("end", (e - t0) / 100), ("life", (e - s) / 100)):
     q = np.percentile(x, [0, 1, 10, 50, 90, 99, 100])
     print(f"{name:6s}", " ".join(f"{v:7.2f}" for v in q))
 hist, edges = np.histogram((e - t0) / 100, bins=20)
 print("end histogram:", list(zip(np.round(edges[:-1], 1).tolist(), hist.tolist())))
 hist, edges = np.histogram((s - t0) / 100, bins=20)
 print("start histogram:", list(zip(np.round(edges[:-1], 1).tolist(), hist.tolist())))
+# the slowest waves' items (one item per wave: g fastest, then window, then keypoint)
+nwin, nhg = (tn + 511) // 512, (hn + 63) // 64
+idx = np.nonzero(buf.view(-1, 4).cpu().numpy()[:, 0] > 0)[0]
+order = np.argsort(e)[::-1][:12]
+for k in order:
+    wv = idx[k]
+    g, rest = wv % nhg, wv // nhg
+    print(f"wave {wv}: v={rest // nwin} w={rest % nwin} g={g}  setup {(su[k] - s[k]) / 100:.2f} loop_end {(f1[k] - s[k]) / 100:.2f} end {(e[k] - t0) / 100:.2f}")

@@ -28,7 +28,7 @@ for s in "$@"; do
             step pmchbm2 600 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d "$PWD/gpurun_out/pmc_write" -o bench -- python3 bench.py --skip-cpu --skip-e2e --steps 20 ;;
     pmcvalu) step pmcvalu 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -T --output-format csv -d "$PWD/gpurun_out/pmc_valu" -o bench -- python3 bench.py --skip-cpu --skip-e2e --steps 20 ;;
     pmcu1v) for v in u1base u1nostore; do PVVOTE_LIB=variants/$v.so step pmcu1_$v 300 rocprofv3 --kernel-include-regex k_vote_bytes --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE -T --output-format csv -d "$PWD/gpurun_out/pmcu1_$v" -o v -- python3 tools/u1_probe.py; done ;;
-    profu1v) for v in u1base u1nostore u1nocomp; do PVVOTE_LIB=variants/$v.so step profu1_$v 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$PWD/gpurun_out/profu1_$v" -o u1 -- python3 tools/u1_probe.py; done ;;
+    profu1v) for v in ${VARIANTS:-u1base u1nostore u1nocomp}; do PVVOTE_LIB=variants/$v.so step profu1_$v 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$PWD/gpurun_out/profu1_$v" -o u1 -- python3 tools/u1_probe.py; done ;;
     profu1x) PVVOTE_DEBUG_BYTES=3 step profu1x 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$PWD/gpurun_out/profu1x" -o u1 -- python3 tools/u1_probe.py ;;
     profu1) step profu1 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$PWD/gpurun_out/profu1" -o u1 -- python3 tools/u1_probe.py ;;
     listpmc) step listpmc 300 rocprofv3 -L ;;
