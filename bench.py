@@ -247,8 +247,8 @@ def measure_u1(dev, hn=512, reps=20):
     inl = torch.empty((hn, VN, tn), dtype=torch.uint8, device=dev)
     rv.voting_for_hypothesis_dense(direct, coords, hyp, inl, 0.99)
     torch.cuda.synchronize()
-    # back-to-back calls between two events: the device time per call (both
-    # kernels of the call: the operand prepass and the byte-output vote)
+    # back-to-back calls between two events: the device time per call (one
+    # kernel, k_vote_bytes, which also makes the pixel operands it stages)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     for _ in range(reps):
@@ -257,8 +257,8 @@ def measure_u1(dev, hn=512, reps=20):
     torch.cuda.synchronize()
     ms = a.elapsed_time(b) / reps
     nbytes = 8 * tn * VN + 8 * tn + 8 * hn * VN + hn * VN * tn      # BASELINE.md U1 algorithmic bytes
-    return dict(kernel="k_prep_api + k_vote_bytes<DENSE> (pv_voting_for_hypothesis)", bytes_per_launch=nbytes,
-                traffic=(pmc_traffic("k_vote_bytes") or 0) + (pmc_traffic("k_prep_api") or 0) or None,
+    return dict(kernel="k_vote_bytes<DENSE> (pv_voting_for_hypothesis)", bytes_per_launch=nbytes,
+                traffic=pmc_traffic("k_vote_bytes"),
                 ms=ms, achieved_gbs=nbytes / (ms * 1e-3) / 1e9, peak_gbs=HBM_PEAK_GBS,
                 frac=nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, hn=hn, tn=tn)
 

@@ -13,9 +13,8 @@
  *   - Every call is asynchronous on `stream` (a hipStream_t; NULL = the null
  *     stream) and performs no host synchronisation, so the calls can be
  *     captured into a hipGraph.  The pipelines allocate nothing (caller
- *     workspace); pv_voting_for_hypothesis, whose reference signature has no
- *     workspace, takes its operand scratch with stream-ordered
- *     hipMallocAsync / hipFreeAsync on `stream`.
+ *     workspace); pv_voting_for_hypothesis needs no scratch at all (one
+ *     kernel reads direct/coords/hypo and writes the mask).
  *   - Return value: 0 on success; a positive hipError_t from the launch; or a
  *     negative PV_E* code for a bad argument.  Nothing ever calls exit()
  *     (the reference's gpuAssert does, cuda_common.h:19-26).
@@ -70,13 +69,6 @@ int pv_generate_hypothesis(const float *direct, const float *coords, const int32
 int pv_voting_for_hypothesis(const float *direct, const float *coords, const float *hypo, uint8_t *inliers,
                              int32_t tn, int32_t vn, int32_t hn, float inlier_thresh, int32_t mode,
                              pv_stream_t stream);
-
-/* the same with caller-owned scratch (no allocation on the stream): workspace of at least
- * pv_voting_for_hypothesis_workspace_size(tn, vn, hn) bytes, device memory, 256-byte aligned. */
-size_t pv_voting_for_hypothesis_workspace_size(int32_t tn, int32_t vn, int32_t hn);
-int pv_voting_for_hypothesis_ws(const float *direct, const float *coords, const float *hypo, uint8_t *inliers,
-                                int32_t tn, int32_t vn, int32_t hn, float inlier_thresh, int32_t mode,
-                                void *workspace, size_t workspace_bytes, pv_stream_t stream);
 
 /* replaces generate_hypothesis_vanishing_point (BND:64-75 -> KU:231-266); hypo f32 [hn,vn,3]. */
 int pv_generate_hypothesis_vp(const float *direct, const float *coords, const int32_t *idxs, float *hypo,

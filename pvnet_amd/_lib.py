@@ -45,9 +45,6 @@ SIGNATURES = [
     ("pv_device_arch", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
     ("pv_generate_hypothesis", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp]),
     ("pv_voting_for_hypothesis", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_i32, c_vp]),
-    ("pv_voting_for_hypothesis_workspace_size", c_size, [c_i32, c_i32, c_i32]),
-    ("pv_voting_for_hypothesis_ws", ctypes.c_int,
-     [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_i32, c_vp, c_size, c_vp]),
     ("pv_generate_hypothesis_vp", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp]),
     ("pv_voting_for_hypothesis_vp", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp]),
     ("pv_vote_counts", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp]),

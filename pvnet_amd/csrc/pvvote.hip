@@ -553,24 +553,25 @@ __device__ __forceinline__ float bcast(float x, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), lane));
 }
 
-// Wave-wide min / max (result in every lane): v_permlane32_swap folds the
-// halves, then xor-swizzles within 32 lanes (no address registers, unlike
-// ds_bpermute).
-template <int XOR>
-__device__ __forceinline__ float swz_xor(float x) {
-    return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x), (XOR << 10) | 0x1f));
+// Wave-wide min / max (result in every lane), all on the VALU: DPP within
+// each row of 16 lanes (quad xor 1, quad xor 2, half-row mirror, row
+// mirror), then v_permlane16_swap and v_permlane32_swap across the rows
+// (no LDS round trips, unlike ds_swizzle / ds_bpermute).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, false));
 }
 template <bool MAX>
 __device__ __forceinline__ float wave_reduce(float x) {
     auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : fminf(a, b); };
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(x), __float_as_int(x), false, false);
-    x = op(__int_as_float(r[0]), __int_as_float(r[1]));
-    x = op(x, swz_xor<16>(x));
-    x = op(x, swz_xor<8>(x));
-    x = op(x, swz_xor<4>(x));
-    x = op(x, swz_xor<2>(x));
-    x = op(x, swz_xor<1>(x));
-    return x;
+    x = op(x, dpp_f<0xB1>(x));    // quad_perm [1,0,3,2]
+    x = op(x, dpp_f<0x4E>(x));    // quad_perm [2,3,0,1]
+    x = op(x, dpp_f<0x141>(x));   // row_half_mirror
+    x = op(x, dpp_f<0x140>(x));   // row_mirror
+    const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_int(x), __float_as_int(x), false, false);
+    x = op(__int_as_float(r16[0]), __int_as_float(r16[1]));
+    const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_int(x), __float_as_int(x), false, false);
+    return op(__int_as_float(r32[0]), __int_as_float(r32[1]));
 }
 __device__ __forceinline__ float wave_min(float x) { return wave_reduce<false>(x); }
 __device__ __forceinline__ float wave_max(float x) { return wave_reduce<true>(x); }
@@ -1563,7 +1564,6 @@ __device__ uint64_t *g_btrace;      // debug build only: per-wave phase stamps o
 #endif
 
 struct ByteArgs {
-    const float4 *prep;    // [vn][tn] (ux, uy, cx, cy), see k_prep_api
     const float *direct;   // [tn][vn][2]
     const float *coords;   // [tn][2]
     const float *hypo;     // [hn][vn][2]
@@ -1571,39 +1571,39 @@ struct ByteArgs {
     int tn, vn, hn, nwin, nhg, fast;
     float thr, tau, gzf, gzr;
     int dbg;               // profiling ablation (PVVOTE_DEBUG_BYTES), 0 = normal
+    int xcd;               // XCD-contiguous item ranges (grid a multiple of 8)
 };
 
-// Operand layouts of the byte-output kernel.  Pixel (t, v): (ux, uy, cx, cy)
-// with u the direction rounded per component; (0, 0) for a pixel that never
-// votes (norm1 < 1e-6 or NaN, KU:119-121, or non-finite coordinates) and
-// ux = NaN for one outside the fast domain.
-__global__ __launch_bounds__(256) void k_prep_api(const float *direct, const float *coords, float4 *prep, int tn,
-                                                  int vn) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t np = (int64_t)vn * tn;
-    if (i < np) {
-        const int v = (int)(i / tn), t = (int)(i - (int64_t)v * tn);
-        const float2 c = *(const float2 *)(coords + (int64_t)t * 2);
-        const float2 d = *(const float2 *)(direct + ((int64_t)t * vn + v) * 2);
-        const float n1 = sqrtf(d.x * d.x + d.y * d.y);
-        const bool ok = !((double)n1 < 1e-6) && n1 == n1 && isfinite(c.x) && isfinite(c.y);
-        const float rs = __builtin_amdgcn_rsqf(fmaf(d.x, d.x, d.y * d.y));
-        float4 q = make_float4(0.f, 0.f, c.x, c.y);
-        if (ok)
-            q = (n1 <= kN1Max) ? make_float4(d.x * rs, d.y * rs, c.x, c.y)
-                               : make_float4(__builtin_nanf(""), 0.f, c.x, c.y);
-        prep[i] = q;
-    }
+// Operands of pixel (t, v) in the byte-output kernel, made where they are
+// staged (no prepass): (ux, uy, cx, cy) with u the direction rounded per
+// component; (0, 0) for a pixel that never votes (norm1 < 1e-6 or NaN,
+// KU:119-121, or non-finite coordinates) and ux = NaN for one outside the
+// fast domain.
+__device__ __forceinline__ float4 api_pixel(const float2 c, const float2 d) {
+    const float n1 = sqrtf(d.x * d.x + d.y * d.y);
+    const bool ok = !((double)n1 < 1e-6) && n1 == n1 && isfinite(c.x) && isfinite(c.y);
+    const float rs = __builtin_amdgcn_rsqf(fmaf(d.x, d.x, d.y * d.y));
+    float4 q = make_float4(0.f, 0.f, c.x, c.y);
+    if (ok)
+        q = (n1 <= kN1Max) ? make_float4(d.x * rs, d.y * rs, c.x, c.y)
+                           : make_float4(__builtin_nanf(""), 0.f, c.x, c.y);
+    return q;
+}
+__device__ __forceinline__ float2 api_coords(const ByteArgs &a, int t) {
+    return *(const float2 *)(a.coords + (int64_t)t * 2);
+}
+__device__ __forceinline__ float2 api_direct(const ByteArgs &a, int t, int v) {
+    return *(const float2 *)(a.direct + ((int64_t)t * a.vn + v) * 2);
 }
 
 // Issue priority from the rows a wave still has (0..3), as in vote_segment:
 // otherwise the SIMD favours its oldest wave, equal shares finish staggered
 // and the last waves of each SIMD run alone at a fraction of the issue rate.
+// (levels 0..2: 3 is the setup's, above every hot loop)
 __device__ __forceinline__ void prio_by_remaining(uint32_t remaining, uint32_t total) {
-    const uint64_t r4 = (uint64_t)remaining * 4, w1 = (uint64_t)total + 1;
-    if (r4 >= 3 * w1) __builtin_amdgcn_s_setprio(3);
-    else if (r4 >= 2 * w1) __builtin_amdgcn_s_setprio(2);
-    else if (r4 >= w1) __builtin_amdgcn_s_setprio(1);
+    const uint64_t r3 = (uint64_t)remaining * 3, w1 = (uint64_t)total + 1;
+    if (r3 >= 2 * w1) __builtin_amdgcn_s_setprio(2);
+    else if (r3 >= w1) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
 }
 
@@ -1611,7 +1611,7 @@ __device__ __forceinline__ void prio_by_remaining(uint32_t remaining, uint32_t t
 template <int MODE>
 __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint8_t *band8, int v, int w, int h0,
                                                int nh, uint32_t rem_after, uint32_t wave_total, uint2 *wq,
-                                               uint32_t &qn, uint64_t *tsetup, const float4 *stage) {
+                                               uint32_t &qn, uint64_t *tsetup, const float4 *stage, float2 hq) {
     const uint32_t qcap = a.dbg == 4 ? 1u : kQueuePerWave;   // (dbg 4: test hook, a full queue)
     const int lane = lane_id();
     const float ntau = -a.tau;
@@ -1622,20 +1622,38 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint
     const uint32_t loff = kBytePix * lane;
 
     // ---- operands: all loads issued together ----
-    float2 hq = make_float2(0.f, 0.f);
-    if (lane < nh) hq = *(const float2 *)(a.hypo + ((int64_t)(h0 + lane) * a.vn + v) * 2);
+    // hq: lane's hypothesis (row h0 + lane), loaded by the caller with the pixels
     uint32_t vmask = 0, okmask = 0;
     bool exo = false;
     float fu[kBytePix], fv[kBytePix], fk1[kBytePix], fk2[kBytePix];   // (ux, uy, cx, cy) first
-    const float4 *pp = a.prep + (int64_t)v * a.tn;
+    if (stage) {   // block-staged window
 #pragma unroll
-    for (int j = 0; j < kBytePix; ++j) {
-        const int t = tb + j;
-        fu[j] = fv[j] = fk1[j] = fk2[j] = 0.f;
-        if (t >= 0 && t < a.tn) {
-            const float4 q = stage ? stage[kBytePix * lane + j] : pp[t];   // (block-staged window, or global)
-            fu[j] = q.x; fv[j] = q.y; fk1[j] = q.z; fk2[j] = q.w;
-            vmask |= 1u << j;
+        for (int j = 0; j < kBytePix; ++j) {
+            const int t = tb + j;
+            fu[j] = fv[j] = fk1[j] = fk2[j] = 0.f;
+            if (t < a.tn) {
+                const float4 q = stage[j * kWave + lane];
+                fu[j] = q.x; fv[j] = q.y; fk1[j] = q.z; fk2[j] = q.w;
+                vmask |= 1u << j;
+            }
+        }
+    } else {       // from the caller's arrays: all 16 loads in flight, then the operands
+        float2 c[kBytePix], d[kBytePix];
+#pragma unroll
+        for (int j = 0; j < kBytePix; ++j) {
+            const int t = tb + j;
+            c[j] = d[j] = make_float2(0.f, 0.f);
+            if (t < a.tn) {
+                c[j] = api_coords(a, t);
+                d[j] = api_direct(a, t, v);
+                vmask |= 1u << j;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kBytePix; ++j) {
+            const float4 q = api_pixel(c[j], d[j]);
+            const bool in = vmask >> j & 1;
+            fu[j] = in ? q.x : 0.f; fv[j] = in ? q.y : 0.f; fk1[j] = in ? q.z : 0.f; fk2[j] = in ? q.w : 0.f;
         }
     }
     if (stage) __syncthreads();   // the staging area is the block's band masks from here on
@@ -1804,7 +1822,7 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint
     };
     uint64_t dmask = 0;                                 // rows with exact work in this kernel (nh <= 64)
     uint32_t lof = loff;                                // (loop-carried through the asm below: no copies)
-    auto row = [&](const F4 &rec, int i, auto partial) {
+    auto row = [&](const F4 &rec, int i, uint32_t &lo, uint32_t &hi) {
         float nz[kBytePix];
 #ifdef PVVOTE_ABLATE_U1_COMPUTE
         float m = 3e38f;
@@ -1813,7 +1831,8 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint
         const float m = zrow(rec, nz);
 #endif
         const uint64_t hit = __builtin_amdgcn_ballot_w64(m <= rec.z);   // flagged rows: rec.z = inf
-        uint32_t lo = pack4(nz[0], nz[1], nz[2], nz[3]), hi = pack4(nz[4], nz[5], nz[6], nz[7]);
+        lo = pack4(nz[0], nz[1], nz[2], nz[3]);
+        hi = pack4(nz[4], nz[5], nz[6], nz[7]);
         bool skip = false;
         if (hit) {
             dmask |= 1ull << i;
@@ -1832,14 +1851,17 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint
                 }
             }
         }
-        // (the row offset is made opaque so that the address stays a scalar
-        // base + 32-bit lane offset instead of a strength-reduced 64-bit VGPR pointer)
-        using gbyte = __attribute__((address_space(1))) uint8_t;
-        gbyte *rowp = (gbyte *)(a.out + (obase + rstep * i));
-        asm volatile("" : "+s"(rowp), "+v"(lof));
 #ifdef PVVOTE_ABLATE_U1_STORE
         if (lo == 0x12345678u && hi == 0x9abcdef0u) skip = false; else skip = true;
 #endif
+        return skip;
+    };
+    using gbyte = __attribute__((address_space(1))) uint8_t;
+    // (the row offset is made opaque so that the address stays a scalar
+    // base + 32-bit lane offset instead of a strength-reduced 64-bit VGPR pointer)
+    auto store_row = [&](int i, uint32_t lo, uint32_t hi, bool skip, auto partial) {
+        gbyte *rowp = (gbyte *)(a.out + (obase + rstep * i));
+        asm volatile("" : "+s"(rowp), "+v"(lof));
         if (!skip) store((uint8_t *)(rowp + lof), lo, hi, partial);
     };
     auto rows = [&](auto partial) {
@@ -1848,11 +1870,18 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint
         for (; i + 1 < nh; i += 2) {
             const F4 rb = recs[i + 1];
             if ((i & 7) == 0) prio_by_remaining(rem_after + (uint32_t)(nh - i), wave_total);
-            row(ra, i, partial);
+            uint32_t lo0, hi0, lo1, hi1;
+            const bool s0 = row(ra, i, lo0, hi0);
             ra = recs[min(i + 2, kByteHB - 1)];
-            row(rb, i + 1, partial);
+            const bool s1 = row(rb, i + 1, lo1, hi1);
+            store_row(i, lo0, hi0, s0, partial);
+            store_row(i + 1, lo1, hi1, s1, partial);
         }
-        if (i < nh) row(ra, i, partial);
+        if (i < nh) {
+            uint32_t lo, hi;
+            const bool sk = row(ra, i, lo, hi);
+            store_row(i, lo, hi, sk, partial);
+        }
     };
     if (__builtin_amdgcn_ballot_w64(vmask != 0xffu)) rows(std::true_type{});
     else rows(std::false_type{});
@@ -1943,7 +1972,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     F4 *recs = recs_all[threadIdx.x / 64];
     uint8_t *band8 = band_all[threadIdx.x / 64];
     uint2 *wq = queue_all[threadIdx.x / 64];
-    const int wave = uniform((int)(blockIdx.x * 4 + threadIdx.x / 64));
+    // setup at the top issue priority, above every hot loop (whose waves
+    // rank 0..2 by the rows they have left, prio_by_remaining): a wave still
+    // in its setup would otherwise wait for them -- and then finish last
+    __builtin_amdgcn_s_setprio(3);
+    int blk = (int)blockIdx.x;
+    if (a.xcd) {
+        // blocks i, i + 8, ... run on one XCD (round-robin dispatch; speed
+        // only, nothing depends on it): give each XCD a contiguous range of
+        // items, whose windows' pixels its L2 then fetches once
+        const int per = (int)gridDim.x / 8;   // (the host pads the grid to a multiple of 8)
+        blk = (blk % 8) * per + blk / 8;
+    }
+    const int wave = uniform(blk * 4 + (int)(threadIdx.x / 64));
 #ifdef PVVOTE_TRACE_U1
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     uint64_t t_setup = 0;
@@ -1952,32 +1993,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     uint64_t *tsetup = nullptr;
 #endif
     const uint32_t nitems = (uint32_t)a.vn * a.nwin * a.nhg;   // < 2^31 (host-checked)
-    // With the hypothesis groups in fours (hn a multiple of 256) a block's
-    // four items share (v, w): the block stages the window's pixels in LDS
-    // once (the band-mask area, free until the hot loop) instead of four
-    // times from L2 -- every item loads at the launch's start at once.
+    // Every load of the wave is issued here, in one round trip at the
+    // launch's start: the item's hypotheses, and the window's pixels.  With
+    // the hypothesis groups in fours (hn a multiple of 256) a block's four
+    // items share (v, w): the block stages the window's pixels in LDS once
+    // (the band-mask area, free until the hot loop) instead of four times.
+    const bool shared = a.nhg % 4 == 0;   // (nitems is then a multiple of 4: every wave has an item)
+    if ((uint32_t)wave >= nitems) return;   // (shared: whole blocks)
+    // items (w, v, g), g fastest: a window's items are adjacent; the last
+    // (partial) window first, so that its slower byte-store rows are not the
+    // launch's tail
+    const uint32_t g = (uint32_t)wave % a.nhg, rest = (uint32_t)wave / a.nhg;
+    const int v = (int)(rest % (uint32_t)a.vn);
+    const int w = (int)((rest / (uint32_t)a.vn + (uint32_t)a.nwin - 1) % (uint32_t)a.nwin);
+    const int h0 = (int)g * kByteHB, nh = min(kByteHB, a.hn - h0);
+    float2 hq = make_float2(0.f, 0.f);
+    if (lane_id() < nh) hq = *(const float2 *)(a.hypo + ((int64_t)(h0 + lane_id()) * a.vn + v) * 2);
     const float4 *stage = nullptr;
-    if (a.nhg % 4 == 0) {
-        // (nitems is then a multiple of 4: every wave of every block has an item)
-        const uint32_t rest = (uint32_t)blockIdx.x * 4 / a.nhg;
-        const int w = (int)(rest % (uint32_t)a.nwin), v = (int)(rest / (uint32_t)a.nwin);
+    if (shared) {
         float4 *st = (float4 *)&band_all[0][0];
-        const float4 *pp = a.prep + (int64_t)v * a.tn;
-        for (int k = threadIdx.x; k < kByteWin; k += 256) {
-            const int t = kByteWin * w + k;
-            if (t < a.tn) st[k] = pp[t];
+        constexpr int kPer = kByteWin / 256;   // pixels per thread; loads first, then the operands
+        float2 c[kPer], d[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int t = kByteWin * w + k * 256 + (int)threadIdx.x;
+            if (t < a.tn) { c[k] = api_coords(a, t); d[k] = api_direct(a, t, v); }
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int t = kByteWin * w + k * 256 + (int)threadIdx.x;
+            // lane-interleaved: lane l's pixel j (k = 8l + j) at j * 64 + l, so
+            // that each of the waves' eight reads is 64 consecutive float4
+            const int kk = k * 256 + (int)threadIdx.x;
+            if (t < a.tn) st[(kk % kBytePix) * kWave + kk / kBytePix] = api_pixel(c[k], d[k]);
         }
         __syncthreads();
         stage = st;
-    } else if ((uint32_t)wave >= nitems) {
-        return;
     }
-    const uint32_t g = (uint32_t)wave % a.nhg, rest = (uint32_t)wave / a.nhg;
-    const int w = (int)(rest % (uint32_t)a.nwin), v = (int)(rest / (uint32_t)a.nwin);
-    const int h0 = (int)g * kByteHB, nh = min(kByteHB, a.hn - h0);
+#ifdef PVVOTE_TRACE_U1
+    const uint64_t t_staged = __builtin_amdgcn_s_memrealtime();
+#endif
     uint32_t qn = 0;
     vote_bytes_seg<MODE>(a, recs, band8, uniform(v), uniform(w), uniform(h0), uniform(nh), 0u, (uint32_t)nh, wq, qn,
-                         tsetup, stage);
+                         tsetup, stage, hq);
 #ifdef PVVOTE_TRACE_U1
     const uint64_t t_first = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1985,12 +2043,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     fix_queued<MODE>(a, wq, qn);
 #ifdef PVVOTE_TRACE_U1
     if (g_btrace && lane_id() == 0) {
-        g_btrace[wave * 4] = t_start;
-        g_btrace[wave * 4 + 1] = t_first;
-        g_btrace[wave * 4 + 2] = __builtin_amdgcn_s_memrealtime();
-        g_btrace[wave * 4 + 3] = t_setup;
+        g_btrace[wave * 8] = t_start;
+        g_btrace[wave * 8 + 1] = t_first;
+        g_btrace[wave * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+        g_btrace[wave * 8 + 3] = t_setup;
+        g_btrace[wave * 8 + 4] = t_staged;
     }
 #endif
+}
+
+// test hook of wave_min / wave_max (pv_debug_wave_minmax)
+__global__ __launch_bounds__(64) void k_debug_minmax(const float *in, float *out) {
+    const float x = in[blockIdx.x * 64 + threadIdx.x];
+    const float mn = wave_min(x), mx = wave_max(x);
+    // every lane must hold the result
+    const bool agree = __builtin_amdgcn_ballot_w64(mn != bcast(mn, 0) || mx != bcast(mx, 0)) == 0;
+    if (threadIdx.x == 0) {
+        out[2 * blockIdx.x] = agree ? mn : __builtin_nanf("");
+        out[2 * blockIdx.x + 1] = agree ? mx : __builtin_nanf("");
+    }
 }
 
 // KU:170-229
@@ -2238,19 +2309,6 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
 
 }  // namespace
 
-namespace {
-// workspace of pv_voting_for_hypothesis_ws: the prepass layout
-struct BytesWs {
-    size_t prep, total;
-};
-BytesWs bytes_ws(int64_t tn, int64_t vn, int64_t hn) {
-    (void)hn;
-    BytesWs w{};
-    w.prep = 0;
-    w.total = align_up((int64_t)sizeof(float4) * vn * tn, 256);
-    return w;
-}
-}  // namespace
 
 // ==========================================================================
 // C ABI
@@ -2294,58 +2352,34 @@ int pv_generate_hypothesis(const float *direct, const float *coords, const int32
 }
 
 
-size_t pv_voting_for_hypothesis_workspace_size(int32_t tn, int32_t vn, int32_t hn) {
-    return (tn <= 0 || vn <= 0 || hn <= 0) ? 0 : bytes_ws(tn, vn, hn).total;
-}
-
-int pv_voting_for_hypothesis_ws(const float *direct, const float *coords, const float *hypo, uint8_t *inliers,
-                                int32_t tn, int32_t vn, int32_t hn, float inlier_thresh, int32_t mode,
-                                void *workspace, size_t workspace_bytes, pv_stream_t stream) {
-    if (!direct || !coords || !hypo || !inliers || tn < 0 || vn <= 0 || hn < 0) return PV_EINVAL;
-    if (mode != PV_VOTE_OR && mode != PV_VOTE_DENSE) return PV_EINVAL;
-    if (tn == 0 || hn == 0) return PV_OK;
-    const BytesWs L = bytes_ws(tn, vn, hn);
-    if (!workspace || workspace_bytes < L.total) return PV_EINVAL;
-    VoteArgs fc{};
-    fast_constants(inlier_thresh, &fc);
-    hipStream_t s = (hipStream_t)stream;
-    char *ws = (char *)workspace;
-    ByteArgs ba{};
-    ba.prep = (const float4 *)(ws + L.prep);
-    ba.direct = direct; ba.coords = coords; ba.hypo = hypo; ba.out = inliers;
-    ba.tn = tn; ba.vn = vn; ba.hn = hn;
-    ba.fast = fc.fast; ba.thr = fc.thr; ba.tau = fc.tau; ba.gzf = fc.gzf; ba.gzr = fc.gzr;
-    ba.nwin = (tn + kByteWin - 1) / kByteWin;
-    ba.nhg = (hn + kByteHB - 1) / kByteHB;
-    if (const char *e3 = getenv("PVVOTE_DEBUG_BYTES")) ba.dbg = atoi(e3);
-    const int64_t nprep = (int64_t)vn * tn;
-    k_prep_api<<<(unsigned)((nprep + 255) / 256), 256, 0, s>>>(direct, coords, (float4 *)(ws + L.prep), tn, vn);
-    const int64_t items = (int64_t)vn * ba.nwin * ba.nhg;
-    if (items >= (1ll << 31)) return PV_EINVAL;   // the kernel's 32-bit item index
-    const unsigned grid = (unsigned)((items + 3) / 4);
-    if (mode == PV_VOTE_DENSE)
-        k_vote_bytes<PV_VOTE_DENSE><<<grid, 256, 0, s>>>(ba);
-    else
-        k_vote_bytes<PV_VOTE_OR><<<grid, 256, 0, s>>>(ba);
-    return last();
-}
-
 int pv_voting_for_hypothesis(const float *direct, const float *coords, const float *hypo, uint8_t *inliers,
                              int32_t tn, int32_t vn, int32_t hn, float inlier_thresh, int32_t mode,
                              pv_stream_t stream) {
     if (!direct || !coords || !hypo || !inliers || tn < 0 || vn <= 0 || hn < 0) return PV_EINVAL;
     if (mode != PV_VOTE_OR && mode != PV_VOTE_DENSE) return PV_EINVAL;
     if (tn == 0 || hn == 0) return PV_OK;
+    VoteArgs fc{};
+    fast_constants(inlier_thresh, &fc);
+    ByteArgs ba{};
+    ba.direct = direct; ba.coords = coords; ba.hypo = hypo; ba.out = inliers;
+    ba.tn = tn; ba.vn = vn; ba.hn = hn;
+    ba.fast = fc.fast; ba.thr = fc.thr; ba.tau = fc.tau; ba.gzf = fc.gzf; ba.gzr = fc.gzr;
+    ba.nwin = (tn + kByteWin - 1) / kByteWin;
+    ba.nhg = (hn + kByteHB - 1) / kByteHB;
+    if (const char *e3 = getenv("PVVOTE_DEBUG_BYTES")) ba.dbg = atoi(e3);
+    const int64_t items = (int64_t)vn * ba.nwin * ba.nhg;
+    if (items >= (1ll << 31)) return PV_EINVAL;   // the kernel's 32-bit item index
+    // one launch, no scratch: the operands are made where the blocks stage them
+    unsigned grid = (unsigned)((items + 3) / 4);
+    ba.xcd = 1;
+    if (const char *e4 = getenv("PVVOTE_BYTES_XCD")) ba.xcd = atoi(e4);
+    if (ba.xcd) grid = (grid + 7) / 8 * 8;
     hipStream_t s = (hipStream_t)stream;
-    // stream-ordered scratch: safe for concurrent streams and graph capture
-    const size_t bytes = pv_voting_for_hypothesis_workspace_size(tn, vn, hn);
-    void *scratch = nullptr;
-    hipError_t e = hipMallocAsync(&scratch, bytes, s);
-    if (e != hipSuccess) return rc(e);
-    int r = pv_voting_for_hypothesis_ws(direct, coords, hypo, inliers, tn, vn, hn, inlier_thresh, mode, scratch,
-                                        bytes, stream);
-    e = hipFreeAsync(scratch, s);
-    return r ? r : rc(e);
+    if (mode == PV_VOTE_DENSE)
+        k_vote_bytes<PV_VOTE_DENSE><<<grid, 256, 0, s>>>(ba);
+    else
+        k_vote_bytes<PV_VOTE_OR><<<grid, 256, 0, s>>>(ba);
+    return last();
 }
 
 int pv_generate_hypothesis_vp(const float *direct, const float *coords, const int32_t *idxs, float *hypo,
@@ -2387,6 +2421,13 @@ int pv_vote_counts(const float *direct, const float *coords, const float *hypo, 
     if (tn == 0) return PV_OK;
     if ((int64_t)vn * va.hgn * tn >= (1ll << 31)) return PV_EINVAL;   // the kernel's 32-bit work index
     launch_vote<false>(va, (int64_t)vn * va.hgn * tn, s);
+    return last();
+}
+
+// debug only (not in pvvote.h): wave min / max of 64 floats per wave -> out[2 * wave + {0, 1}]
+int pv_debug_wave_minmax(const float *in, float *out, int32_t nwaves, pv_stream_t stream) {
+    if (!in || !out || nwaves <= 0) return PV_EINVAL;
+    k_debug_minmax<<<(unsigned)nwaves, 64, 0, (hipStream_t)stream>>>(in, out);
     return last();
 }
 

@@ -97,12 +97,9 @@ def _voting(direct, coords, hypo_pts, inliers, thr, mode):
         return
     L = _lib.load()
     with torch.cuda.device(direct.device):
-        # scratch from torch's caching allocator (stream-ordered like the tensors themselves)
-        ws = torch.empty(L.pv_voting_for_hypothesis_workspace_size(tn, vn, hn), dtype=torch.uint8,
-                         device=direct.device)
-        _lib.check(L.pv_voting_for_hypothesis_ws(direct.data_ptr(), coords.data_ptr(), hypo_pts.data_ptr(),
-                                                 inliers.data_ptr(), tn, vn, hn, float(thr), mode, ws.data_ptr(),
-                                                 ws.numel(), _stream(direct.device)), "voting_for_hypothesis")
+        _lib.check(L.pv_voting_for_hypothesis(direct.data_ptr(), coords.data_ptr(), hypo_pts.data_ptr(),
+                                              inliers.data_ptr(), tn, vn, hn, float(thr), mode,
+                                              _stream(direct.device)), "voting_for_hypothesis")
 
 
 def generate_hypothesis_vanishing_point(direct, coords, idxs) -> torch.Tensor:

@@ -44,6 +44,30 @@ def test_native_library_is_the_gfx950_build(device):
     assert buf.value.decode().startswith("gfx950"), buf.value
 
 
+def test_wave_min_max_reduction(device):
+    """The DPP / permlane wave reduction the vote kernels' guard bands rest on
+    (debug export, not in pvvote.h): every lane gets the min and max."""
+    import ctypes
+    from pvnet_amd import _lib
+    L = _lib.load()
+    fn = L.pv_debug_wave_minmax
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal((256, 64)).astype(np.float32) * 100
+    for k in range(64):                  # the extreme in every lane position
+        x[k, k] = 1e6
+        x[64 + k, k] = -1e6
+    x[128, 5] = np.nan                   # fminf / fmaxf skip NaN
+    x[129, :] = 3.0
+    xd = cu(x, device)
+    out = torch.empty((256, 2), dtype=torch.float32, device=device)
+    assert fn(xd.data_ptr(), out.data_ptr(), 256, torch.cuda.current_stream(device).cuda_stream) == 0
+    got = out.cpu().numpy()
+    np.testing.assert_array_equal(got[:, 0], np.nanmin(x, 1))
+    np.testing.assert_array_equal(got[:, 1], np.nanmax(x, 1))
+
+
 # ---------------------------------------------------------------- kernels
 @pytest.mark.parametrize("case", ["cat_v3_512", "synth_v3_512"])
 def test_generate_and_vote_kernels_bit_exact(case, device, rv):

@@ -24,18 +24,18 @@ direct = torch.from_numpy(np.ascontiguousarray(
 idxs = torch.randint(0, tn, (hn, VN, 2), dtype=torch.int32, device="cuda")
 hyp = rv.generate_hypothesis(direct, coords, idxs)
 inl = torch.empty((hn, VN, tn), dtype=torch.uint8, device="cuda")
-buf = torch.zeros(65536 * 4, dtype=torch.int64, device="cuda")
+buf = torch.zeros(65536 * 8, dtype=torch.int64, device="cuda")
 for it in range(4):
     buf.zero_()
     L.pv_debug_set_bytes_trace(ctypes.c_void_p(buf.data_ptr() if it == 3 else 0))
     rv.voting_for_hypothesis_dense(direct, coords, hyp, inl, 0.99)
     torch.cuda.synchronize()
-t = buf.view(-1, 4).cpu().numpy()
+t = buf.view(-1, 8).cpu().numpy()
 t = t[t[:, 0] > 0]
-s, f1, e, su = t[:, 0], t[:, 1], t[:, 2], t[:, 3]
+s, f1, e, su, stg = t[:, 0], t[:, 1], t[:, 2], t[:, 3], t[:, 4]
 t0 = s.min()
 print("waves", len(t), "span us", (e.max() - t0) / 100.0)
-for name, x in (("start", (s - t0) / 100), ("setup", (su - s) / 100), ("first", (f1 - s) / 100),
+for name, x in (("start", (s - t0) / 100), ("staged", (stg - s) / 100), ("setup", (su - s) / 100), ("first", (f1 - s) / 100),
                 ("end", (e - t0) / 100), ("life", (e - s) / 100)):
     q = np.percentile(x, [0, 1, 10, 50, 90, 99, 100])
     print(f"{name:6s}", " ".join(f"{v:7.2f}" for v in q))
@@ -45,9 +45,9 @@ hist, edges = np.histogram((s - t0) / 100, bins=20)
 print("start histogram:", list(zip(np.round(edges[:-1], 1).tolist(), hist.tolist())))
 # the slowest waves' items (one item per wave: g fastest, then window, then keypoint)
 nwin, nhg = (tn + 511) // 512, (hn + 63) // 64
-idx = np.nonzero(buf.view(-1, 4).cpu().numpy()[:, 0] > 0)[0]
+idx = np.nonzero(buf.view(-1, 8).cpu().numpy()[:, 0] > 0)[0]
 order = np.argsort(e)[::-1][:12]
 for k in order:
     wv = idx[k]
     g, rest = wv % nhg, wv // nhg
-    print(f"wave {wv}: v={rest // nwin} w={rest % nwin} g={g}  setup {(su[k] - s[k]) / 100:.2f} loop_end {(f1[k] - s[k]) / 100:.2f} end {(e[k] - t0) / 100:.2f}")
+    print(f"wave {wv}: v={rest % VN} w={(rest // VN + nwin - 1) % nwin} g={g}  setup {(su[k] - s[k]) / 100:.2f} loop_end {(f1[k] - s[k]) / 100:.2f} end {(e[k] - t0) / 100:.2f}")
