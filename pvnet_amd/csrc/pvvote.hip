@@ -657,11 +657,11 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
     // arbiter otherwise favours the oldest wave, so equal shares finish
     // staggered and the last waves run alone; this keeps them level.
     // (q = 4 * remaining / (wave_total + 1), compared instead of divided)
+    // (levels 0..2: 3 is the prologue's, above every hot loop)
     auto set_prio = [&](int64_t remaining) {
-        const int64_t r4 = remaining * 4, w1 = wave_total + 1;
-        if (r4 >= 3 * w1) __builtin_amdgcn_s_setprio(3);
-        else if (r4 >= 2 * w1) __builtin_amdgcn_s_setprio(2);
-        else if (r4 >= w1) __builtin_amdgcn_s_setprio(1);
+        const int64_t r3 = remaining * 3, w1 = wave_total + 1;
+        if (r3 >= 2 * w1) __builtin_amdgcn_s_setprio(2);
+        else if (r3 >= w1) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
     };
     const float tau = a.tau;
@@ -1013,6 +1013,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     const int64_t nunits = SH ? (int64_t)gridDim.x : (int64_t)gridDim.x * 4;
     const int gpu = SH ? 4 : 1;           // hypothesis groups per unit
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    // the prologue (hypotheses, first sub-chunk) at the top issue priority:
+    // the hot loops rank 0..2 by the work they have left (set_prio), and a
+    // wave still in its prologue would otherwise wait behind them
+    __builtin_amdgcn_s_setprio(3);
     __shared__ VoteSlab<PREPPED> slab_all[SH ? 2 : 4];
     __shared__ QuarterBoxes qb_all[SH ? 2 : 1];
     VoteSlab<PREPPED> *slabs = SH ? slab_all : slab_all + threadIdx.x / 64;
@@ -1045,10 +1049,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     }
     if (a.trace && lane_id() == 0) {
         uint32_t hw;
+        uint32_t xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
         a.trace[wave * 4] = t_start;
         a.trace[wave * 4 + 1] = __builtin_amdgcn_s_memrealtime();
-        a.trace[wave * 4 + 2] = hw;
+        a.trace[wave * 4 + 2] = ((uint64_t)xcc << 32) | hw;
         a.trace[wave * 4 + 3] = ((uint64_t)nseg << 32) | (uint32_t)nfix;
     }
 }

@@ -11,7 +11,7 @@ for rep in 1 2; do
 import json, sys
 l = [x for x in open(sys.argv[2]) if x.startswith("{")][-1]
 d = json.loads(l)
-print(repr(sys.argv[1]), "img/s", d["value"], "vote_us", round(d["roofline"]["avg_kernel_ms"] * 1000, 2), "lat_us", round(d["latency_ms_per_image"] * 1000, 1))
+print(repr(sys.argv[1]), "img/s", d["value"], "vote_us", round(d["roofline_vote_count"]["avg_kernel_ms"] * 1000, 2), "lat_us", round(d["latency_ms_per_image"] * 1000, 1))
 PY
   done
 done

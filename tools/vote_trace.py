@@ -37,6 +37,16 @@ for name, x in (("start", s_us), ("end", e_us), ("life", life)):
 cu = (hw >> 8) & 0xF
 se = (hw >> 13) & 0x7
 print("start by SE:", [f"{np.median(s_us[se == k]):.2f}" for k in range(8) if (se == k).any()])
+xcc = (hw >> 32) & 0xF
+print("life by XCC (median, p90, max):", [f"{k}: {np.median(life[xcc == k]):.2f} {np.percentile(life[xcc == k], 90):.2f} {life[xcc == k].max():.2f}" for k in range(8) if (xcc == k).any()])
+cuid = xcc * 64 + se * 16 + cu
+per_cu = {c: np.median(life[cuid == c]) for c in np.unique(cuid)}
+v = np.array(list(per_cu.values()))
+print("per-CU median life: min %.2f p10 %.2f p50 %.2f p90 %.2f max %.2f (%d CUs)" % (v.min(), *np.percentile(v, [10, 50, 90]), v.max(), len(v)))
+simd = (hw >> 4) & 3
+wid_in = cuid * 4 + simd
+cnt = np.bincount(np.unique(wid_in, return_inverse=True)[1])
+print("waves per SIMD: min", cnt.min(), "max", cnt.max())
 hist, edges = np.histogram(s_us, bins=20)
 print("start histogram:", hist.tolist(), "edges", np.round(edges[[0, -1]], 2).tolist())
 hist, edges = np.histogram(e_us, bins=20)
