@@ -152,6 +152,54 @@ int pv_estimate_voting_distribution_with_mean(const pv_image_desc *img, const pv
 int pv_estimate_voting_distribution(const pv_image_desc *img, const pv_vote_params *prm, float *mean,
                                     float *cov, void *workspace, size_t workspace_bytes, pv_stream_t stream);
 
+/* ---- uncertainty-weighted PnP (the consumer of the EVD covariances), batched ---- */
+
+#define PV_PNP_WEIGHTS 0   /* wgt: f64 [pn,3] (wxx, wxy, wyy) per image, as uncertainty_pnp() takes them */
+#define PV_PNP_COV 1       /* wgt: f32 [pn,2,2] covariances -> inv(sqrtm(C)), 0 if C00 < 1e-6 or NaN
+                            * (lib/utils/evaluation_utils.py:168-178), then uncertainty_pnp() */
+#define PV_PNP_COV_V2 2    /* wgt: f32 [pn,2,2] -> isotropic 1 / max eig(C), 0 if C00 < 1e-5
+                            * (uncertainty_pnp_v2, extend_utils.py:116-166) */
+
+typedef struct pv_pnp_batch {
+    int32_t b, pn;          /* images; points per image (4 <= pn <= 64) */
+    int32_t mode;           /* PV_PNP_* */
+    const float *pts2d;     /* [b][pn][2] image points (the voted keypoints) */
+    const void *wgt;        /* see PV_PNP_*; [b][pn][...] */
+    const double *pts3d;    /* [pn][3] model points, image i at pts3d + i * pts3d_stride */
+    const double *K;        /* [3][3] camera matrix, image i at K + i * K_stride */
+    int64_t pts3d_stride;   /* elements; 0 = one set shared by the batch */
+    int64_t K_stride;       /* elements; 0 = shared */
+} pv_pnp_batch;
+
+/* optional device outputs (any may be NULL) */
+typedef struct pv_pnp_diag {
+    double *init_rt;        /* [b][6] the P3P initial pose (rvec, t) */
+    int32_t *p3p_ok;        /* [b] 1 if P3P found a solution (cv2.solvePnP's return value) */
+    int32_t *iterations;    /* [b] trust-region iterations */
+    int32_t *status;        /* [b] PV_PNP_STOP_* */
+    double *cost;           /* [b] final 0.5 * sum r^2 */
+} pv_pnp_diag;
+
+#define PV_PNP_STOP_GRADIENT 1
+#define PV_PNP_STOP_PARAMETER 2
+#define PV_PNP_STOP_FUNCTION 3
+#define PV_PNP_STOP_MAX_ITER 4
+#define PV_PNP_STOP_RADIUS 5
+#define PV_PNP_STOP_P3P_ONLY 6  /* pn == 4: the P3P pose is the result (extend_utils.py:90-94) */
+
+/* replaces extend_utils.uncertainty_pnp / uncertainty_pnp_v2 (extend_utils.py:63-166): per image the
+ * P3P pose of the four highest-weight points (cv2.solvePnP SOLVEPNP_P3P: points 0..2 solve, point 3
+ * picks), then the weighted reprojection least squares of src/uncertainty_pnp.cpp:7-92 by Ceres 2.0's
+ * Levenberg-Marquardt (restated).  Rt out f64 [b][3][4] = [Rodrigues(r) | t].  One wave per
+ * image, fp64. */
+int pv_uncertainty_pnp(const pv_pnp_batch *batch, double *Rt, const pv_pnp_diag *diag, pv_stream_t stream);
+
+/* replaces the C entry uncertainty_pnp(pts2d, pts3d, wgt2d, K, init_rt, result_rt, pn)
+ * (src/uncertainty_pnp.cpp:58-92): the least squares alone from given initial poses.
+ * init_rt / result_rt f64 [b][6] (angle-axis, translation); mode must be PV_PNP_WEIGHTS. */
+int pv_uncertainty_pnp_refine(const pv_pnp_batch *batch, const double *init_rt, double *result_rt,
+                              const pv_pnp_diag *diag, pv_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

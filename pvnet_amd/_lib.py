@@ -16,6 +16,8 @@ LIB_PATH = os.environ.get("PVVOTE_LIB", os.path.join(HERE, "libpvvote.so"))
 PV_MASK_I64, PV_MASK_U8, PV_MASK_I32, PV_MASK_SEG_F32, PV_MASK_SEG_F16 = 0, 1, 2, 3, 4
 PV_VERTEX_F32, PV_VERTEX_F16 = 0, 1
 PV_VOTE_OR, PV_VOTE_DENSE = 0, 1
+PV_PNP_WEIGHTS, PV_PNP_COV, PV_PNP_COV_V2 = 0, 1, 2
+PNP_STOP = {1: "gradient", 2: "parameter", 3: "function", 4: "max_iterations", 5: "radius", 6: "p3p_only"}
 
 c_i32, c_i64, c_u64, c_f32, c_size, c_vp = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                             ctypes.c_size_t, ctypes.c_void_p)
@@ -36,6 +38,15 @@ class VoteParams(ctypes.Structure):
 class V3Diag(ctypes.Structure):
     _fields_ = [("hyp", c_vp), ("counts", c_vp), ("win_idx", c_vp), ("win_ratio", c_vp), ("tn", c_vp),
                 ("iters", c_vp), ("ata", c_vp), ("atb", c_vp), ("ev_vote_begin", c_vp), ("ev_vote_end", c_vp)]
+
+
+class PnpBatch(ctypes.Structure):
+    _fields_ = [("b", c_i32), ("pn", c_i32), ("mode", c_i32), ("pts2d", c_vp), ("wgt", c_vp), ("pts3d", c_vp),
+                ("K", c_vp), ("pts3d_stride", c_i64), ("K_stride", c_i64)]
+
+
+class PnpDiag(ctypes.Structure):
+    _fields_ = [("init_rt", c_vp), ("p3p_ok", c_vp), ("iterations", c_vp), ("status", c_vp), ("cost", c_vp)]
 
 
 # (name, restype, argtypes) -- one entry per function declared in include/pvvote.h
@@ -59,6 +70,9 @@ SIGNATURES = [
      [ctypes.POINTER(ImageDesc), ctypes.POINTER(VoteParams), c_vp, c_vp, c_vp, c_size, c_vp]),
     ("pv_estimate_voting_distribution", ctypes.c_int,
      [ctypes.POINTER(ImageDesc), ctypes.POINTER(VoteParams), c_vp, c_vp, c_vp, c_size, c_vp]),
+    ("pv_uncertainty_pnp", ctypes.c_int, [ctypes.POINTER(PnpBatch), c_vp, ctypes.POINTER(PnpDiag), c_vp]),
+    ("pv_uncertainty_pnp_refine", ctypes.c_int,
+     [ctypes.POINTER(PnpBatch), c_vp, c_vp, ctypes.POINTER(PnpDiag), c_vp]),
 ]
 
 _lib = None

@@ -15,6 +15,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "pvvote.hip")
+SRCS = [SRC, os.path.join(HERE, "csrc", "pvpnp.hip")]
 HDR = os.path.join(REPO, "include", "pvvote.h")
 OUT = os.path.join(HERE, "libpvvote.so")
 ARCH = os.environ.get("PVVOTE_ARCH", "gfx950")
@@ -48,12 +49,12 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(p) > t for p in (SRC, HDR, __file__))
+    return any(os.path.getmtime(p) > t for p in (*SRCS, HDR, __file__))
 
 
 def build(force: bool = False, extra=()) -> str:
     if force or needs_build():
-        cmd = [hipcc(), *HIPCC_FLAGS, *extra, "-o", OUT + ".tmp", SRC]
+        cmd = [hipcc(), *HIPCC_FLAGS, *extra, "-o", OUT + ".tmp", *SRCS]
         subprocess.check_call(cmd)
         os.replace(OUT + ".tmp", OUT)
     return OUT

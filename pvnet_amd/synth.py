@@ -26,12 +26,14 @@ def disk_mask(H=480, W=640, center=(320.0, 240.0), radius=97.5):
 
 
 def synthetic_field(seed=1234, H=480, W=640, vn=9, radius=97.5, center=(320.0, 240.0),
-                    noise=0.05, outlier=0.2, scale_jitter=False, mask=None, dtype=np.float32):
+                    noise=0.05, outlier=0.2, scale_jitter=False, mask=None, dtype=np.float32, keypoints=None):
     """S(seed): returns dict(seg [1,2,H,W], vertex [1,2vn,H,W], mask [H,W] bool,
     keypoints [vn,2] float64).  numpy ``default_rng(seed)`` only."""
     rng = np.random.default_rng(seed)
     m = disk_mask(H, W, center, radius) if mask is None else np.asarray(mask, bool)
     kps = rng.uniform([200.0, 120.0], [440.0, 360.0], size=(vn, 2))
+    if keypoints is not None:      # e.g. projected model keypoints (the PnP tests)
+        kps = np.asarray(keypoints, np.float64).reshape(vn, 2)
     rows, cols = np.nonzero(m)
     tn = rows.shape[0]
     ang = np.arctan2(kps[None, :, 1] - rows[:, None], kps[None, :, 0] - cols[:, None])  # [tn,vn]
