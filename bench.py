@@ -297,6 +297,50 @@ def measure_batch(dev, b=32, hn=512, steps=10):
                      "the CPU oracle lands within 0.1 px of the same values (parity: tests/)")
 
 
+def measure_pnp(dev, b=1024, reps=10, cpu_images=8):
+    """configs[4]'s last stage: uncertainty PnP (pv_uncertainty_pnp, one wave
+    per image, fp64) on b synthetic LINEMOD-camera images of 9 box keypoints
+    with anisotropic covariances; timed with hipEvents over `reps` launches.
+    Beside it the CPU oracle (oracle/pnp.py: the same P3P + Ceres-LM
+    restatement in numpy) on a small sample, images/s."""
+    from pvnet_amd import extend_utils as eu
+    rng = np.random.default_rng(0)
+    K = np.array([[572.4114, 0.0, 325.2611], [0.0, 573.57043, 242.04899], [0.0, 0.0, 1.0]])
+    p3 = np.concatenate([np.array([[x, y, z] for x in (-1, 1) for y in (-1, 1) for z in (-1, 1)]) * 0.05,
+                         np.zeros((1, 3))])
+    p2 = np.empty((b, 9, 2), np.float32)
+    cov = np.empty((b, 9, 2, 2), np.float32)
+    for i in range(b):
+        a = rng.normal(size=3)
+        th = np.linalg.norm(a)
+        k = a / th
+        kx = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+        R = np.eye(3) + np.sin(th) * kx + (1 - np.cos(th)) * kx @ kx
+        X = p3 @ R.T + np.array([rng.uniform(-0.1, 0.1), rng.uniform(-0.1, 0.1), rng.uniform(0.6, 1.0)])
+        m = rng.normal(size=(9, 2, 2))
+        cov[i] = m @ m.transpose(0, 2, 1) + 0.05 * np.eye(2)
+        p2[i] = np.stack([K[0, 0] * X[:, 0] / X[:, 2] + K[0, 2], K[1, 1] * X[:, 1] / X[:, 2] + K[1, 2]], 1) \
+            + rng.normal(size=(9, 2)) * 0.5
+    tp2, tcov = torch.from_numpy(p2).to(dev), torch.from_numpy(cov).to(dev)
+    tp3, tK = torch.from_numpy(p3).to(dev), torch.from_numpy(K).to(dev)
+    eu.uncertainty_pnp_batch(tp2, tcov, tp3, tK)
+    torch.cuda.synchronize()
+    a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        eu.uncertainty_pnp_batch(tp2, tcov, tp3, tK)
+    e.record()
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(e) / reps
+    from oracle import pnp as P
+    t0 = time.perf_counter()
+    for i in range(cpu_images):
+        P.uncertainty_pnp(p2[i], P.weights_from_cov(cov[i]), p3, K)
+    cpu = cpu_images / (time.perf_counter() - t0)
+    return dict(images_per_s=round(b / (ms * 1e-3), 1), ms_per_batch=round(ms, 4), batch=b, keypoints=9,
+                cpu_oracle_images_per_s=round(cpu, 2), cpu_sample=f"{cpu_images} images, 1 thread, numpy")
+
+
 def measure_e2e(dev, half=False, iters=20):
     """configs[1] (fp32) / configs[2]'s fp16 backbone: ResNet-18 seg+vector-
     field forward (PyTorch-ROCm, MIOpen, channels_last) + the HIP v3 layer
@@ -448,6 +492,10 @@ def report(args, ws, res, final_err, seg, ver, fb, rvg, work, dev):
             line["voting_config2_batch32"] = measure_batch(dev)
         except Exception as e:
             line["voting_config2_batch32"] = {"error": repr(e)}
+        try:
+            line["pnp_config5"] = measure_pnp(dev)
+        except Exception as e:
+            line["pnp_config5"] = {"error": repr(e)}
     if ws == 1 and not args.skip_cpu:
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     print(json.dumps(line), flush=True)
