@@ -750,7 +750,9 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
                 const float cx = q.x - ox, cy = q.y - oy;
                 const float k1 = fmaf(q.z, cx, q.w * cy);
                 const float k2 = fmaf(q.z, cy, -(q.w * cx));
-                stage[t] = F4{q.z, q.w, -k1, -k2};
+                // a pixel that never votes (prep: cx NaN; the slab's padding):
+                // u = 0, -k1 = -1e30 -> z = -1e30 tau < 0 and far outside the band
+                stage[t] = q.x == q.x ? F4{q.z, q.w, -k1, -k2} : F4{0.f, 0.f, -1.0e30f, 0.f};
             }
             if (wid * kWave < np) {
                 const float mn = wave_min(xl), mx = wave_max(xh);
@@ -851,7 +853,7 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
             const float cx = q.x - ox, cy = q.y - oy;          // exact for pixel centres
             const float k1 = fmaf(q.z, cx, q.w * cy);          // NaN for invalid pixels
             const float k2 = fmaf(q.z, cy, -(q.w * cx));
-            stage[k * kWave + lane] = F4{q.z, q.w, -k1, -k2};
+            stage[k * kWave + lane] = q.x == q.x ? F4{q.z, q.w, -k1, -k2} : F4{0.f, 0.f, -1.0e30f, 0.f};
         }
         __builtin_amdgcn_wave_barrier();
         }
@@ -898,12 +900,14 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
                     for (int k = 1; k < kHypLane; ++k) {
                         if (i == k) { hxi = hx[k]; hyi = hy[k]; gdi = gd[k]; ex = he[k].x; ey = he[k].y; }
                     }
-                    const bool u = fabsf(zval(stage[j + p], hxi, hyi)) <= gdi;
+                    const float zz = zval(stage[j + p], hxi, hyi);
+                    const bool u = fabsf(zz) <= gdi;
                     if (__builtin_amdgcn_ballot_w64(u)) {
                         const F4 e = stagex.get(j + p);
                         const int r = (u && exact_vote(e.z, e.w, e.x, e.y, ex, ey, a.thr)) ? 1 : 0;
+                        const int f = (u && !signbit(zz)) ? 1 : 0;   // what the sign count took
 #pragma unroll
-                        for (int k = 0; k < kHypLane; ++k) cnt[k] += i == k ? r : 0;
+                        for (int k = 0; k < kHypLane; ++k) cnt[k] += i == k ? r - f : 0;
                     }
                 }
             };
@@ -911,19 +915,33 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
             // into two named buffers (no register copies).  The band is checked
             // once per step on min |z| per hypothesis (v_min ignores NaN, so
             // invalid pixels and non-fast hypotheses never trigger it).
+            // The fast count is a sign count: v_perm gathers the sign bytes
+            // (0xff / 0x00) of 4 z values and v_sad_u8 adds them, 255 per
+            // negative z -- 1 VALU op per pair instead of a compare and an
+            // add-with-carry.  Pairs inside the band are re-decided by
+            // fix_step, which also takes back what the sign count gave them.
+            uint32_t neg[kHypLane];
+#pragma unroll
+            for (int i = 0; i < kHypLane; ++i) neg[i] = 0;
             auto step = [&](F4 q0, F4 q1, F4 q2, F4 q3, int j) {
                 float m[kHypLane];
 #pragma unroll
                 for (int i = 0; i < kHypLane; ++i) m[i] = kBig;
                 const F4 *qs[4] = {&q0, &q1, &q2, &q3};
+                float z[4][kHypLane];
 #pragma unroll
                 for (int p = 0; p < 4; ++p) {
 #pragma unroll
                     for (int i = 0; i < kHypLane; ++i) {
-                        const float z = zval(*qs[p], hx[i], hy[i]);
-                        cnt[i] += z > gd[i];
-                        m[i] = fminf(m[i], fabsf(z));
+                        z[p][i] = zval(*qs[p], hx[i], hy[i]);
+                        m[i] = fminf(m[i], fabsf(z[p][i]));
                     }
+                }
+#pragma unroll
+                for (int i = 0; i < kHypLane; ++i) {
+                    const uint32_t p01 = __builtin_amdgcn_perm(__float_as_uint(z[1][i]), __float_as_uint(z[0][i]), 0x0c0c0b09u);
+                    const uint32_t p23 = __builtin_amdgcn_perm(__float_as_uint(z[3][i]), __float_as_uint(z[2][i]), 0x0b090c0cu);
+                    neg[i] = __builtin_amdgcn_sad_u8(p01 | p23, 0u, neg[i]);
                 }
                 bool hit = false;
 #pragma unroll
@@ -933,8 +951,8 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
                     fix_step(j);
                 }
             };
-            // the slab past np holds NaN pixels (never counted, never in the
-            // band), so the loop runs whole 8-pixel iterations
+            // the slab past np holds never-voting pixels (negative z, never in
+            // the band), so the loop runs whole 8-pixel iterations
 #ifdef PVVOTE_ABLATE_LOOP
             const int nit = 0;
 #else
@@ -953,6 +971,10 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
                 a0 = stage[jn]; a1 = stage[jn + 1]; a2 = stage[jn + 2]; a3 = stage[jn + 3];
                 step(b0, b1, b2, b3, j + 4);
             }
+            // positives = pairs stepped - negatives (never-voting pixels and the
+            // padding are negative); hypotheses outside the fast test count 0 here
+#pragma unroll
+            for (int i = 0; i < kHypLane; ++i) cnt[i] += hf[i] ? 8 * nit - (int)(neg[i] / 255u) : 0;
             // exact-only hypotheses (rare): lane = pixel, one hypothesis at a time
 #pragma unroll
             for (int i = 0; i < kHypLane; ++i) {

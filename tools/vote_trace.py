@@ -64,3 +64,16 @@ for q in (0.1, 0.5, 0.9, 0.99):
 top = order[-50:]
 print("slowest 50: nfix mean", nfix[top].mean(), "nseg mean", nseg[top].mean(), " | all: nfix mean", nfix.mean(), "nseg mean", nseg.mean())
 print("corr(life, nfix)", np.corrcoef(life, nfix)[0, 1], "corr(life, nseg)", np.corrcoef(life, nseg)[0, 1])
+# per-SIMD: when its first and last wave end (equal work per wave: a wide
+# gap means unfair issue within the SIMD, a wide spread of last ends means
+# SIMDs of different speed)
+first_end, last_end = [], []
+for sid in np.unique(wid_in):
+    e = e_us[wid_in == sid]
+    first_end.append(e.min())
+    last_end.append(e.max())
+first_end, last_end = np.array(first_end), np.array(last_end)
+print("per-SIMD last end: p10 %.2f p50 %.2f p90 %.2f max %.2f" % (*np.percentile(last_end, [10, 50, 90]), last_end.max()))
+print("per-SIMD first end: p10 %.2f p50 %.2f p90 %.2f" % tuple(np.percentile(first_end, [10, 50, 90])))
+gap = last_end - first_end
+print("per-SIMD last-first gap: p10 %.2f p50 %.2f p90 %.2f max %.2f" % (*np.percentile(gap, [10, 50, 90]), gap.max()))
