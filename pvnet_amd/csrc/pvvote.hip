@@ -650,7 +650,8 @@ struct QuarterBoxes {
 // quarter boxes come through LDS.
 template <bool PREPPED, bool SH>
 __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED> *slabs, QuarterBoxes *qbs, int &buf, int b, int v, int hg,
-                                             int ts, int te, int n, int64_t rem_after, int64_t wave_total, int &nfix) {
+                                             int ts, int te, int n, int64_t rem_after, int64_t wave_total, int &nfix,
+                                             uint64_t &tloop) {
     const int lane = lane_id();
     const int wid = SH ? (int)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave) : 0;
     // Issue priority from the work this wave still has (0..3): the SIMD's
@@ -914,7 +915,7 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
             // 4 pixels x kHypLane hypotheses per step, LDS reads one step ahead
             // into two named buffers (no register copies).  The band is checked
             // once per step on min |z| per hypothesis (v_min ignores NaN, so
-            // invalid pixels and non-fast hypotheses never trigger it).
+            // non-fast hypotheses never trigger it).
             // The fast count is a sign count: v_perm gathers the sign bytes
             // (0xff / 0x00) of 4 z values and v_sad_u8 adds them, 255 per
             // negative z -- 1 VALU op per pair instead of a compare and an
@@ -959,6 +960,7 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
             const int nit = (np + 7) >> 3;
 #endif
             F4 a0 = stage[0], a1 = stage[1], a2 = stage[2], a3 = stage[3];
+            if (a.trace && tloop == 0) tloop = __builtin_amdgcn_s_memrealtime();   // (debug traces only)
             for (int it = 0; it < nit; ++it) {
                 const int j = it * 8;
                 if ((j & (kWave - 1)) == 0) {
@@ -1051,6 +1053,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     even_share(total, (uint32_t)nunits, (uint32_t)unit, &lo, &hi);
     const int64_t wave_total = hi - lo;
     int nfix = 0, nseg = 0;   // diagnostics (trace)
+    uint64_t tloop = 0;       // (trace) first hot-loop entry
     // walk the segments of [lo, hi)
     int b = 0;
     uint32_t base = 0;
@@ -1065,7 +1068,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         const int v = g / ggn, gg = g - v * ggn;
         const int hg = SH ? gg * 4 + (int)__builtin_amdgcn_readfirstlane(threadIdx.x / 64) : gg;
         vote_segment<PREPPED, SH>(a, slabs, qb_all, buf, uniform(b), uniform(v), uniform(hg), uniform(ts), uniform(te), n,
-                                       (int64_t)(hi - lo) - (te - ts), wave_total, nfix);
+                                       (int64_t)(hi - lo) - (te - ts), wave_total, nfix, tloop);
         lo += te - ts;
         ++nseg;
     }
@@ -1074,10 +1077,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         uint32_t xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        a.trace[wave * 4] = t_start;
-        a.trace[wave * 4 + 1] = __builtin_amdgcn_s_memrealtime();
-        a.trace[wave * 4 + 2] = ((uint64_t)xcc << 32) | hw;
-        a.trace[wave * 4 + 3] = ((uint64_t)nseg << 32) | (uint32_t)nfix;
+        a.trace[wave * 8] = t_start;
+        a.trace[wave * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+        a.trace[wave * 8 + 2] = ((uint64_t)xcc << 32) | hw;
+        a.trace[wave * 8 + 3] = ((uint64_t)nseg << 32) | (uint32_t)nfix;
+        a.trace[wave * 8 + 4] = tloop;
     }
 }
 

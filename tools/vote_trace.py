@@ -16,13 +16,13 @@ L.pv_debug_set_vote_trace.argtypes = [ctypes.c_void_p]
 f = synth.synthetic_field(1234)
 seg = torch.from_numpy(f["seg"]).cuda()
 vert = torch.from_numpy(f["vertex"]).cuda()
-buf = torch.zeros(16384 * 4, dtype=torch.int64, device="cuda")
+buf = torch.zeros(16384 * 8, dtype=torch.int64, device="cuda")
 for it in range(4):
     buf.zero_()
     L.pv_debug_set_vote_trace(ctypes.c_void_p(buf.data_ptr()) if it else None)
     ransac_voting_layer_v3_from_network(seg, vert, 512)
     torch.cuda.synchronize()
-t = buf.view(-1, 4).cpu().numpy()
+t = buf.view(-1, 8).cpu().numpy()
 t = t[t[:, 0] > 0]
 s, e, hw = t[:, 0], t[:, 1], t[:, 2]
 nfix, nseg = t[:, 3] & 0xffffffff, t[:, 3] >> 32
@@ -30,6 +30,8 @@ t0 = s.min()
 s_us, e_us = (s - t0) / 100.0, (e - t0) / 100.0
 life = e_us - s_us
 print("waves", len(t), "span us", e_us.max())
+tl = (t[:, 4] - t0) / 100.0
+print("first hot loop at (us): p10 %.2f p50 %.2f p90 %.2f max %.2f" % (*np.percentile(tl - s_us, [10, 50, 90]), (tl - s_us).max()))
 for name, x in (("start", s_us), ("end", e_us), ("life", life)):
     q = np.percentile(x, [0, 1, 10, 50, 90, 99, 100])
     print(f"{name:6s}", " ".join(f"{v:7.2f}" for v in q))
