@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=1, help="images per GPU per step (configs[1]: batch=1)")
     ap.add_argument("--hn", type=int, default=512, help="round_hyp_num (DEMO:55 / TRAIN:141)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--inflight", type=int, default=4,
+    ap.add_argument("--inflight", type=int, default=8,
                     help="images in flight: consecutive steps alternate over this many HIP streams (own workspaces)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--skip-cpu", action="store_true")
