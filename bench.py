@@ -341,6 +341,70 @@ def measure_pnp(dev, b=1024, reps=10, cpu_images=8):
                 cpu_oracle_images_per_s=round(cpu, 2), cpu_sample=f"{cpu_images} images, 1 thread, numpy")
 
 
+def measure_pose(dev, b=32, steps=5):
+    """configs[4]'s path on the device, keypoints -> covariances -> poses:
+    ransac_voting_layer_v3 + estimate_voting_distribution_with_mean (16
+    rounds x 256 hypotheses) + uncertainty PnP, for a batch of b synthetic
+    fields whose 9 keypoints are a 10 cm box projected by the LINEMOD camera
+    at random poses; captured as one hipGraph, `steps` replays timed."""
+    from pvnet_amd import extend_utils as eu
+    from pvnet_amd import ransac_voting_gpu as rvg
+    from pvnet_amd import synth
+    rng = np.random.default_rng(3)
+    K = np.array([[572.4114, 0.0, 325.2611], [0.0, 573.57043, 242.04899], [0.0, 0.0, 1.0]])
+    # 8 box corners + an off-centre ninth point (a centred one is collinear
+    # with opposite corners: P3P has no solution on such triples)
+    p3 = np.concatenate([np.array([[x, y, z] for x in (-1, 1) for y in (-1, 1) for z in (-1, 1)]) * 0.05,
+                         np.array([[0.012, -0.017, 0.009]])])
+    fs, ts = [], []
+    for i in range(b):
+        a = rng.normal(size=3) * 0.4
+        th = np.linalg.norm(a)
+        k = a / th
+        kx = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+        R = np.eye(3) + np.sin(th) * kx + (1 - np.cos(th)) * kx @ kx
+        t = np.array([rng.uniform(-0.05, 0.05), rng.uniform(-0.05, 0.05), rng.uniform(0.7, 0.9)])
+        X = p3 @ R.T + t
+        kp = np.stack([K[0, 0] * X[:, 0] / X[:, 2] + K[0, 2], K[1, 1] * X[:, 1] / X[:, 2] + K[1, 2]], 1)
+        c = kp[8]
+        fs.append(synth.synthetic_field(700 + i, keypoints=kp, center=(float(c[0]), float(c[1]))))
+        ts.append(t)
+    seg = torch.from_numpy(np.concatenate([f["seg"] for f in fs])).to(dev)
+    ver = torch.from_numpy(np.concatenate([f["vertex"] for f in fs])).to(dev)
+    bb, c2, h, w = ver.shape
+    vertex = ver.permute(0, 2, 3, 1).view(bb, h, w, c2 // 2, 2)
+    mask = seg.argmax(1)
+    tp3, tK = torch.from_numpy(p3).to(dev), torch.from_numpy(K).to(dev)
+    w1, w2 = rvg.VotingWorkspace(), rvg.VotingWorkspace()
+
+    def once():
+        mean = rvg.ransac_voting_layer_v3(mask, vertex, 512, _workspace=w1, _seed=11)
+        mean, cov = rvg.estimate_voting_distribution_with_mean(mask, vertex, mean, _workspace=w2, _seed=12)
+        return eu.uncertainty_pnp_batch(mean, cov, tp3, tK, mode="cov", diag=pd)
+    pd = {}
+    s = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(s):
+        Rt = once()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            Rt = once()
+    g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.replay()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    terr = np.abs(Rt.cpu().numpy()[:, :, 3] - np.array(ts)).max(1)
+    return dict(images_per_s=round(b / dt, 1), ms_per_batch=round(dt * 1e3, 4), batch=b,
+                max_translation_err_m=round(float(terr.max()), 5), median_translation_err_m=round(float(np.median(terr)), 5),
+                p3p_ok=int(pd["p3p_ok"].sum()), pnp_status=np.bincount(pd["status"].cpu().numpy(), minlength=7).tolist(),
+                stages="v3 (hn 512) + EVD with mean (16 x 256 hypotheses) + uncertainty PnP (P3P + LM), one hipGraph",
+                note="synthetic box-keypoint fields (0.05 rad noise, 20% outliers); error vs the generating pose")
+
+
 def measure_e2e(dev, half=False, iters=20):
     """configs[1] (fp32) / configs[2]'s fp16 backbone: ResNet-18 seg+vector-
     field forward (PyTorch-ROCm, MIOpen, channels_last) + the HIP v3 layer
@@ -496,6 +560,10 @@ def report(args, ws, res, final_err, seg, ver, fb, rvg, work, dev):
             line["pnp_config5"] = measure_pnp(dev)
         except Exception as e:
             line["pnp_config5"] = {"error": repr(e)}
+        try:
+            line["pose_config5_batch32"] = measure_pose(dev)
+        except Exception as e:
+            line["pose_config5_batch32"] = {"error": repr(e)}
     if ws == 1 and not args.skip_cpu:
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     print(json.dumps(line), flush=True)
