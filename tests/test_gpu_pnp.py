@@ -151,3 +151,24 @@ def test_input_checks(device, eu):
     with pytest.raises(RuntimeError, match="init_rt needs"):
         eu.uncertainty_pnp_batch(p2, torch.zeros((2, 9, 2, 2), device=device), box_keypoints(), K_LM,
                                  init_rt=torch.zeros((2, 6), device=device))
+
+
+def test_demo_cat_pose_from_the_references_evd(device, eu):
+    """The reference's EVD output on the demo cat (golden) -> device PnP ->
+    the demo's ground-truth pose; and the same from the device's own EVD
+    with the golden idxs injected (v3 mean from the golden keypoints)."""
+    from pvnet_amd import ransac_voting_gpu as rvg
+    from tests import golden_io as G
+    g = G.load("cat_evdm")
+    mean = torch.from_numpy(g["mean"]).to(device)
+    cov = torch.from_numpy(g["cov"]).to(device)
+    Rt = eu.pose_from_voting(mean, cov, g["points_3d"], K_LM).cpu().numpy()[0]
+    np.testing.assert_allclose(Rt, P.uncertainty_pnp(g["mean"][0], P.weights_from_cov(g["cov"][0]), g["points_3d"],
+                                                     K_LM), atol=TOL)
+    np.testing.assert_allclose(Rt, g["pose"], atol=2e-5)
+    mask, vertex, _ = G.cat_inputs(g)
+    idxs = g["idxs"][0].reshape(1, -1, 9, 2)
+    m2, c2 = rvg.estimate_voting_distribution_with_mean(torch.from_numpy(mask).to(device),
+                                                        torch.from_numpy(vertex).to(device), mean, _idxs=idxs)
+    Rt2 = eu.pose_from_voting(m2, c2, g["points_3d"], K_LM).cpu().numpy()[0]
+    np.testing.assert_allclose(Rt2, g["pose"], atol=2e-5)

@@ -131,3 +131,20 @@ def test_four_points_is_the_p3p_pose():
     Rt = P.uncertainty_pnp(p2[:4], w, p3[:4], K_LM)
     np.testing.assert_allclose(Rt[:, :3], R, atol=1e-6)
     np.testing.assert_allclose(Rt[:, 3], t, atol=1e-6)
+
+
+def test_demo_cat_pose_from_the_references_evd():
+    """Known answer from the reference's own data: its EVD-with-mean output on
+    the demo cat (tests/golden/cat_evdm.npz, made by ransac_voting_gpu.py) with
+    the demo's 3-D keypoints -> the demo's ground-truth pose (data/demo
+    cat_pose.npy).  The first keypoint's covariance is below the 1e-6 gate
+    (zero weight, evaluation_utils.py:171)."""
+    from tests import golden_io as G
+    g = G.load("cat_evdm")
+    mean, cov = g["mean"][0], g["cov"][0]
+    assert cov[0, 0, 0] < 1e-6
+    d = {}
+    Rt = P.uncertainty_pnp(mean, P.weights_from_cov(cov), g["points_3d"], K_LM, diag=d)
+    assert d["p3p_ok"]
+    np.testing.assert_allclose(Rt, g["pose"], atol=2e-5)
+    np.testing.assert_allclose(P.uncertainty_pnp_v2(mean, cov, g["points_3d"], K_LM), g["pose"], atol=2e-5)
