@@ -230,7 +230,7 @@ def _raw_v3(rvg, seg, ver, hn, seed, work, out, dd):
     return out
 
 
-def measure_u1(dev, hn=512, reps=20):
+def measure_u1(dev, hn=512, reps=100):
     """API-faithful voting_for_hypothesis (dense u8 [hn,vn,tn] write) on one
     S(1234) image: the kernel the north star's HBM roofline names (U1)."""
     from pvnet_amd import ransac_voting as rv
@@ -247,8 +247,13 @@ def measure_u1(dev, hn=512, reps=20):
     inl = torch.empty((hn, VN, tn), dtype=torch.uint8, device=dev)
     rv.voting_for_hypothesis_dense(direct, coords, hyp, inl, 0.99)
     torch.cuda.synchronize()
-    # back-to-back calls between two events: the device time per call (one
-    # kernel, k_vote_bytes, which also makes the pixel operands it stages)
+    # back-to-back calls between two events on the launching stream, queued
+    # ahead of the device (the host issues a call in well under the kernel's
+    # time): the device time per call, the dispatch gaps between kernels
+    # included.  (Events between the calls would add their own packets'
+    # gaps; rocprof's kernel durations exclude both.)
+    for _ in range(4):
+        rv.voting_for_hypothesis_dense(direct, coords, hyp, inl, 0.99)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     for _ in range(reps):
@@ -538,8 +543,8 @@ def report(args, ws, res, final_err, seg, ver, fb, rvg, work, dev):
                                     traffic=u1["traffic"], avg_kernel_ms=round(u1["ms"], 5),
                                     bytes_per_launch=u1["bytes_per_launch"], hn=u1["hn"], tn=u1["tn"],
                                     note="algorithmic bytes 8*tn*vn + 8*tn + 8*hn*vn + hn*vn*tn (SURVEY 8(d) U1) "
-                                         "per launch / mean launch time from hipEvents around back-to-back "
-                                         "calls on the launching stream (launch gaps included); traffic = "
+                                         "per launch / mean launch time from hipEvents around 100 back-to-back calls on the "
+                                         "launching stream (dispatch gaps between the kernels included); traffic = "
                                          "2*FETCH_SIZE + WRITE_SIZE per launch (profiles/r01_pmc_traffic.json)")
         except Exception as e:  # reported, never hides the main number
             line["roofline"] = {"error": repr(e)}

@@ -1639,37 +1639,58 @@ __device__ __forceinline__ void prio_by_remaining(uint32_t remaining, uint32_t t
     else __builtin_amdgcn_s_setprio(0);
 }
 
+// A window's fast-test frame, shared by the waves that vote it: origin o
+// (an integer point), the voting pixels' bounding box relative to o and its
+// radius R >= |c - o|; slow = some pixel is outside the fast domain.
+struct WinInfo {
+    float ox, oy, bxl, bxh, byl, byh, Rw;
+    int slow;
+};
+
 // rows h0 + i, i < nh (<= kByteHB), of keypoint v, pixels of window w
 template <int MODE>
 __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint8_t *band8, int v, int w, int h0,
-                                               int nh, uint32_t rem_after, uint32_t wave_total, uint2 *wq,
-                                               uint32_t &qn, uint64_t *tsetup, const float4 *stage, float2 hq) {
+                                               int nh, uint32_t rem_after, uint32_t wave_total, uint16_t *wq,
+                                               uint32_t &qn, uint64_t *tsetup, const float4 *stage, float2 hq,
+                                               const float4 *raw, const float2 *hraw, const WinInfo *win) {
     const uint32_t qcap = a.dbg == 4 ? 1u : kQueuePerWave;   // (dbg 4: test hook, a full queue)
     const int lane = lane_id();
     const float ntau = -a.tau;
     const int tb = kByteWin * w + kBytePix * lane;              // lane's first pixel
     const int64_t rstep = (int64_t)a.vn * a.tn;                 // R(h + 1) - R(h)
     // row i's bytes of this lane: wave-uniform offset (SGPRs) + 32-bit lane offset
-    const int64_t obase = ((int64_t)h0 * a.vn + v) * a.tn + (int64_t)kByteWin * w;
+    int64_t obase = ((int64_t)h0 * a.vn + v) * a.tn + (int64_t)kByteWin * w;
+    obase = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(obase >> 32)) << 32 |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((int)obase));   // (SGPRs for the asm below)
     const uint32_t loff = kBytePix * lane;
 
-    // ---- operands: all loads issued together ----
+    // ---- operands ----
     // hq: lane's hypothesis (row h0 + lane), loaded by the caller with the pixels
-    uint32_t vmask = 0, okmask = 0;
-    bool exo = false;
-    float fu[kBytePix], fv[kBytePix], fk1[kBytePix], fk2[kBytePix];   // (ux, uy, cx, cy) first
-    if (stage) {   // block-staged window
+    uint32_t vmask = 0;
+    float fu[kBytePix], fv[kBytePix], fk1[kBytePix], fk2[kBytePix];
+    float ox = 0.f, oy = 0.f, Rw = 0.f, bxl = 0.f, bxh = 0.f, byl = 0.f, byh = 0.f;
+    bool slow;
+    if (stage) {
+        // block-staged window: the fast operands and the window's bounds are
+        // made once per block (stage_window); pixels past tn never vote
 #pragma unroll
         for (int j = 0; j < kBytePix; ++j) {
-            const int t = tb + j;
-            fu[j] = fv[j] = fk1[j] = fk2[j] = 0.f;
-            if (t < a.tn) {
+            fu[j] = fv[j] = fk2[j] = 0.f;
+            fk1[j] = -1.0e30f;
+            if (tb + j < a.tn) {
                 const float4 q = stage[j * kWave + lane];
                 fu[j] = q.x; fv[j] = q.y; fk1[j] = q.z; fk2[j] = q.w;
                 vmask |= 1u << j;
             }
         }
-    } else {       // from the caller's arrays: all 16 loads in flight, then the operands
+        slow = __builtin_amdgcn_readfirstlane(!a.fast || win->slow);
+        ox = win->ox; oy = win->oy; Rw = win->Rw;
+        bxl = win->bxl; bxh = win->bxh; byl = win->byl; byh = win->byh;
+        __syncthreads();   // the staging area is the block's band masks from here on
+    } else {
+        // from the caller's arrays: all 16 loads in flight, then the operands
+        uint32_t okmask = 0;
+        bool exo = false;
         float2 c[kBytePix], d[kBytePix];
 #pragma unroll
         for (int j = 0; j < kBytePix; ++j) {
@@ -1687,51 +1708,49 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint
             const bool in = vmask >> j & 1;
             fu[j] = in ? q.x : 0.f; fv[j] = in ? q.y : 0.f; fk1[j] = in ? q.z : 0.f; fk2[j] = in ? q.w : 0.f;
         }
-    }
-    if (stage) __syncthreads();   // the staging area is the block's band masks from here on
 #pragma unroll
-    for (int j = 0; j < kBytePix; ++j) {
-        exo |= fu[j] != fu[j];                                  // outside the fast domain
-        if (fu[j] != 0.f || fv[j] != 0.f) okmask |= 1u << j;    // votes at all
-    }
-    const bool slow = __builtin_amdgcn_readfirstlane(!a.fast || __builtin_amdgcn_ballot_w64(exo) != 0);
-    // origin: an integer point at the first voting pixel; the voting pixels'
-    // bounding box relative to it (R >= |c - o|, and D >= |h - c| per row)
-    const uint64_t anyok = __builtin_amdgcn_ballot_w64(okmask != 0);
-    float ox = 0.f, oy = 0.f, Rw = 0.f, bxl = 0.f, bxh = 0.f, byl = 0.f, byh = 0.f;
-    if (anyok) {
-        const int l0 = __builtin_ctzll(anyok);
-        const int j0 = __builtin_ctz(__builtin_amdgcn_readlane(okmask, l0));
-        float fx = fk1[0], fy = fk2[0];
+        for (int j = 0; j < kBytePix; ++j) {
+            exo |= fu[j] != fu[j];                                  // outside the fast domain
+            if (fu[j] != 0.f || fv[j] != 0.f) okmask |= 1u << j;    // votes at all
+        }
+        slow = __builtin_amdgcn_readfirstlane(!a.fast || __builtin_amdgcn_ballot_w64(exo) != 0);
+        // origin: an integer point at the first voting pixel; the voting pixels'
+        // bounding box relative to it (R >= |c - o|, and D >= |h - c| per row)
+        const uint64_t anyok = __builtin_amdgcn_ballot_w64(okmask != 0);
+        if (anyok) {
+            const int l0 = __builtin_ctzll(anyok);
+            const int j0 = __builtin_ctz(__builtin_amdgcn_readlane(okmask, l0));
+            float fx = fk1[0], fy = fk2[0];
 #pragma unroll
-        for (int j = 1; j < kBytePix; ++j)
-            if (j == j0) { fx = fk1[j]; fy = fk2[j]; }
-        ox = floorf(bcast(fx, l0));
-        oy = floorf(bcast(fy, l0));
-        float xl = 3.0e38f, xh = -3.0e38f, yl = 3.0e38f, yh = -3.0e38f;
+            for (int j = 1; j < kBytePix; ++j)
+                if (j == j0) { fx = fk1[j]; fy = fk2[j]; }
+            ox = floorf(bcast(fx, l0));
+            oy = floorf(bcast(fy, l0));
+            float xl = 3.0e38f, xh = -3.0e38f, yl = 3.0e38f, yh = -3.0e38f;
 #pragma unroll
-        for (int j = 0; j < kBytePix; ++j)
-            if (okmask >> j & 1) {
-                xl = fminf(xl, fk1[j] - ox); xh = fmaxf(xh, fk1[j] - ox);
-                yl = fminf(yl, fk2[j] - oy); yh = fmaxf(yh, fk2[j] - oy);
-            }
-        bxl = wave_min(xl); bxh = wave_max(xh);
-        byl = wave_min(yl); byh = wave_max(yh);
-        const float ax = fmaxf(-bxl, bxh), ay = fmaxf(-byl, byh);
-        Rw = __builtin_amdgcn_sqrtf(fmaf(ax, ax, ay * ay)) * 1.00001f;
-    }
-    // fast operands (ux, uy, -k1, -k2) relative to the origin, in place;
-    // pixels that never vote get u = 0, -k1 = -1e30: -z = 1e30 tau, far
-    // above the band, for every finite h'
+            for (int j = 0; j < kBytePix; ++j)
+                if (okmask >> j & 1) {
+                    xl = fminf(xl, fk1[j] - ox); xh = fmaxf(xh, fk1[j] - ox);
+                    yl = fminf(yl, fk2[j] - oy); yh = fmaxf(yh, fk2[j] - oy);
+                }
+            bxl = wave_min(xl); bxh = wave_max(xh);
+            byl = wave_min(yl); byh = wave_max(yh);
+            const float ax = fmaxf(-bxl, bxh), ay = fmaxf(-byl, byh);
+            Rw = __builtin_amdgcn_sqrtf(fmaf(ax, ax, ay * ay)) * 1.00001f;
+        }
+        // fast operands (ux, uy, -k1, -k2) relative to the origin, in place;
+        // pixels that never vote get u = 0, -k1 = -1e30: -z = 1e30 tau, far
+        // above the band, for every finite h'
 #pragma unroll
-    for (int j = 0; j < kBytePix; ++j) {
-        const bool ok = okmask >> j & 1;
-        const float ux = fu[j], uy = fv[j];
-        const float cx = fk1[j] - ox, cy = fk2[j] - oy;
-        fu[j] = ok ? ux : 0.f;
-        fv[j] = ok ? uy : 0.f;
-        fk1[j] = ok ? -fmaf(ux, cx, uy * cy) : -1.0e30f;
-        fk2[j] = ok ? -fmaf(ux, cy, -(uy * cx)) : 0.f;
+        for (int j = 0; j < kBytePix; ++j) {
+            const bool ok = okmask >> j & 1;
+            const float ux = fu[j], uy = fv[j];
+            const float cx = fk1[j] - ox, cy = fk2[j] - oy;
+            fu[j] = ok ? ux : 0.f;
+            fv[j] = ok ? uy : 0.f;
+            fk1[j] = ok ? -fmaf(ux, cx, uy * cy) : -1.0e30f;
+            fk2[j] = ok ? -fmaf(ux, cy, -(uy * cx)) : 0.f;
+        }
     }
     // hypothesis records (lane i -> row h0 + 8i): h - o, band, exact flag
     uint64_t flagged;                                   // rows the exact pass decides whole
@@ -1841,12 +1860,12 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint
         }
         const uint32_t base = qn;
         qn = min(base + tot, qcap);
-        const uint32_t r = (uint32_t)((h0 + i) * a.vn + v);
         uint32_t k = base + pre;
 #pragma unroll
         for (int j = 0; j < kBytePix; ++j) {
             if (bm >> j & 1) {
-                if (k < qcap) wq[k] = make_uint2(r, (uint32_t)(tb + j));
+                // (row in the wave's batch, pixel in the window): 6 + 9 bits
+                if (k < qcap) wq[k] = (uint16_t)(i << 9 | (kBytePix * lane + j));
                 ++k;
             }
         }
@@ -1892,7 +1911,10 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint
     // (the row offset is made opaque so that the address stays a scalar
     // base + 32-bit lane offset instead of a strength-reduced 64-bit VGPR pointer)
     auto store_row = [&](int i, uint32_t lo, uint32_t hi, bool skip, auto partial) {
-        gbyte *rowp = (gbyte *)(a.out + (obase + rstep * i));
+        uint64_t rp = (uint64_t)(a.out + (obase + rstep * i));
+        rp = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(rp >> 32)) << 32 |
+             (uint32_t)__builtin_amdgcn_readfirstlane((int)rp);
+        gbyte *rowp = (gbyte *)rp;
         asm volatile("" : "+s"(rowp), "+v"(lof));
         if (!skip) store((uint8_t *)(rowp + lof), lo, hi, partial);
     };
@@ -1939,15 +1961,20 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint
             const int t = tb + j;
             ec[j] = ed[j] = make_float2(0.f, 0.f);
             if (vmask >> j & 1) {
-                ec[j] = *(const float2 *)(a.coords + (int64_t)t * 2);
-                ed[j] = *(const float2 *)(a.direct + ((int64_t)t * a.vn + v) * 2);
+                if (raw) {
+                    const float4 r = raw[j * kWave + lane];
+                    ec[j] = make_float2(r.x, r.y);
+                    ed[j] = make_float2(r.z, r.w);
+                } else {
+                    ec[j] = *(const float2 *)(a.coords + (int64_t)t * 2);
+                    ed[j] = *(const float2 *)(a.direct + ((int64_t)t * a.vn + v) * 2);
+                }
             }
         }
         while (dmask) {
             const int i = __builtin_ctzll(dmask);
             dmask &= dmask - 1;
-            const int h = h0 + i;
-            const float2 q = *(const float2 *)(a.hypo + ((int64_t)h * a.vn + v) * 2);
+            const float2 q = hraw[i];
             uint8_t *p = a.out + (obase + rstep * i) + loff;
             if ((flagged >> i) & 1) {
                 uint32_t lo = 0, hi = 0;
@@ -1975,20 +2002,30 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint
 }
 
 // A wave's queued band pairs, decided by the reference's sequence at its
-// end: lane = entry, the three operand loads of up to 64 pairs in flight at
-// once; the byte goes over the wave's own earlier fast guess (dense, program
-// order) or is set (OR).
+// end: lane = entry; the operands are the reference's own (c, d, h) -- from
+// the block's raw window in LDS when it is staged (no memory round trip at
+// the wave's end), else loaded, up to 64 pairs in flight at once; the byte
+// goes over the wave's own earlier fast guess (dense, program order) or is
+// set (OR).
 template <int MODE>
-__device__ __forceinline__ void fix_queued(const ByteArgs &a, const uint2 *wq, uint32_t qn) {
+__device__ __forceinline__ void fix_queued(const ByteArgs &a, const uint16_t *wq, uint32_t qn, int v, int w, int h0,
+                                           const float4 *raw, const float2 *hraw) {
     for (uint32_t k = lane_id(); k < qn; k += kWave) {
-        const uint2 e = wq[k];
-        const uint32_t r = e.x, t = e.y;
-        const uint32_t v = r % (uint32_t)a.vn;
-        const float2 q = *(const float2 *)(a.hypo + (int64_t)r * 2);
-        const float2 c = *(const float2 *)(a.coords + (int64_t)t * 2);
-        const float2 d = *(const float2 *)(a.direct + ((int64_t)t * a.vn + v) * 2);
+        const uint32_t e = wq[k];
+        const uint32_t i = e >> 9, p = e & (kByteWin - 1);
+        const uint32_t t = (uint32_t)(kByteWin * w) + p;
+        const float2 q = hraw[i];
+        float2 c, d;
+        if (raw) {
+            const float4 r = raw[(p % kBytePix) * kWave + p / kBytePix];
+            c = make_float2(r.x, r.y);
+            d = make_float2(r.z, r.w);
+        } else {
+            c = *(const float2 *)(a.coords + (int64_t)t * 2);
+            d = *(const float2 *)(a.direct + ((int64_t)t * a.vn + v) * 2);
+        }
         const bool in = exact_vote(d.x, d.y, c.x, c.y, q.x, q.y, a.thr);
-        uint8_t *o = a.out + (int64_t)r * a.tn + t;
+        uint8_t *o = a.out + ((int64_t)(h0 + (int)i) * a.vn + v) * a.tn + t;
         if (MODE == PV_VOTE_DENSE) *o = in ? 1 : 0;
         else if (in) *o = 1;
     }
@@ -1996,14 +2033,19 @@ __device__ __forceinline__ void fix_queued(const ByteArgs &a, const uint2 *wq, u
 
 // One item per wave: (keypoint v, window w, hypothesis group g of kByteHB),
 // g fastest; a wave beyond the items exits.
-template <int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_vote_bytes(ByteArgs a) {
-    __shared__ F4 recs_all[4][kByteHB];
-    __shared__ alignas(16) uint8_t band_all[4][kByteHB * kWave];   // per deferred row: each lane's band-pair mask
-    __shared__ uint2 queue_all[4][kQueuePerWave];          // per wave: queued band pairs (row, pixel)
+template <int MODE, int WPB>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_vote_bytes(ByteArgs a) {
+    __shared__ F4 recs_all[WPB][kByteHB];
+    __shared__ alignas(16) uint8_t band_all[WPB][kByteHB * kWave];   // per deferred row: each lane's band-pair mask
+    __shared__ uint16_t queue_all[WPB][kQueuePerWave];     // per wave: queued band pairs (row, pixel)
+    __shared__ float2 hraw_all[WPB][kByteHB];              // per wave: its rows' hypotheses
+    __shared__ float4 raw_win[WPB == 4 ? kByteWin : 1];    // block-staged window: (c, d) as given
+    __shared__ float4 win_part[WPB];                       // per wave: its pixels' bounds (staging)
+    __shared__ int win_exo[WPB];
     F4 *recs = recs_all[threadIdx.x / 64];
     uint8_t *band8 = band_all[threadIdx.x / 64];
-    uint2 *wq = queue_all[threadIdx.x / 64];
+    uint16_t *wq = queue_all[threadIdx.x / 64];
+    float2 *hraw = hraw_all[threadIdx.x / 64];
     // setup at the top issue priority, above every hot loop (whose waves
     // rank 0..2 by the rows they have left, prio_by_remaining): a wave still
     // in its setup would otherwise wait for them -- and then finish last
@@ -2016,7 +2058,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         const int per = (int)gridDim.x / 8;   // (the host pads the grid to a multiple of 8)
         blk = (blk % 8) * per + blk / 8;
     }
-    const int wave = uniform(blk * 4 + (int)(threadIdx.x / 64));
+    const int wave = uniform(blk * WPB + (int)(threadIdx.x / 64));
 #ifdef PVVOTE_TRACE_U1
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     uint64_t t_setup = 0;
@@ -2030,7 +2072,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     // the hypothesis groups in fours (hn a multiple of 256) a block's four
     // items share (v, w): the block stages the window's pixels in LDS once
     // (the band-mask area, free until the hot loop) instead of four times.
-    const bool shared = a.nhg % 4 == 0;   // (nitems is then a multiple of 4: every wave has an item)
+    // (nitems is then a multiple of 4: every wave has an item)
+    const bool shared = WPB == 4 && a.nhg % 4 == 0;
     if ((uint32_t)wave >= nitems) return;   // (shared: whole blocks)
     // items (w, v, g), g fastest: a window's items are adjacent; the last
     // (partial) window first, so that its slower byte-store rows are not the
@@ -2041,38 +2084,86 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     const int h0 = (int)g * kByteHB, nh = min(kByteHB, a.hn - h0);
     float2 hq = make_float2(0.f, 0.f);
     if (lane_id() < nh) hq = *(const float2 *)(a.hypo + ((int64_t)(h0 + lane_id()) * a.vn + v) * 2);
-    const float4 *stage = nullptr;
-    if (shared) {
+    hraw[lane_id()] = hq;
+    const float4 *stage = nullptr, *raw = nullptr;
+    WinInfo wi{};
+    if (WPB == 4 && shared) {
+        // the block's window, once: raw (c, d) for the exact decisions, the
+        // fast operands (ux, uy, -k1, -k2) relative to the window's origin
+        // (the floor of its first pixel), and the voting pixels' bounds
         float4 *st = (float4 *)&band_all[0][0];
         constexpr int kPer = kByteWin / 256;   // pixels per thread; loads first, then the operands
+        const int t0 = kByteWin * w;
         float2 c[kPer], d[kPer];
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
-            const int t = kByteWin * w + k * 256 + (int)threadIdx.x;
+            const int t = t0 + k * 256 + (int)threadIdx.x;
             if (t < a.tn) { c[k] = api_coords(a, t); d[k] = api_direct(a, t, v); }
         }
+        const float2 c0 = api_coords(a, t0);
+        const bool obad = !(isfinite(c0.x) && isfinite(c0.y));
+        const float ox = obad ? 0.f : floorf(c0.x), oy = obad ? 0.f : floorf(c0.y);
+        float xl = 3.0e38f, xh = -3.0e38f, yl = 3.0e38f, yh = -3.0e38f;
+        bool exo = false;
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
-            const int t = kByteWin * w + k * 256 + (int)threadIdx.x;
+            const int t = t0 + k * 256 + (int)threadIdx.x;
             // lane-interleaved: lane l's pixel j (k = 8l + j) at j * 64 + l, so
             // that each of the waves' eight reads is 64 consecutive float4
             const int kk = k * 256 + (int)threadIdx.x;
-            if (t < a.tn) st[(kk % kBytePix) * kWave + kk / kBytePix] = api_pixel(c[k], d[k]);
+            if (t < a.tn) {
+                const float4 q = api_pixel(c[k], d[k]);
+                const bool ok = q.x != 0.f || q.y != 0.f;   // votes at all (NaN: outside the fast domain)
+                exo |= q.x != q.x;
+                const float cx = q.z - ox, cy = q.w - oy;
+                float4 f = make_float4(0.f, 0.f, -1.0e30f, 0.f);   // never votes: -z = 1e30 tau
+                if (ok) {
+                    f = make_float4(q.x, q.y, -fmaf(q.x, cx, q.y * cy), -fmaf(q.x, cy, -(q.y * cx)));
+                    xl = fminf(xl, cx); xh = fmaxf(xh, cx);
+                    yl = fminf(yl, cy); yh = fmaxf(yh, cy);
+                }
+                st[(kk % kBytePix) * kWave + kk / kBytePix] = f;
+                raw_win[(kk % kBytePix) * kWave + kk / kBytePix] = make_float4(c[k].x, c[k].y, d[k].x, d[k].y);
+            }
+        }
+        xl = wave_min(xl); xh = wave_max(xh);
+        yl = wave_min(yl); yh = wave_max(yh);
+        const bool wexo = __builtin_amdgcn_ballot_w64(exo) != 0;
+        if (lane_id() == 0) {
+            win_part[threadIdx.x / 64] = make_float4(xl, xh, yl, yh);
+            win_exo[threadIdx.x / 64] = wexo;
         }
         __syncthreads();
+        float4 p = win_part[0];
+        int ex = win_exo[0];
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+            const float4 q = win_part[k];
+            p.x = fminf(p.x, q.x); p.y = fmaxf(p.y, q.y);
+            p.z = fminf(p.z, q.z); p.w = fmaxf(p.w, q.w);
+            ex |= win_exo[k];
+        }
+        wi.slow = ex | obad;
+        wi.ox = ox; wi.oy = oy;
+        if (p.x <= p.y) {   // some pixel votes
+            wi.bxl = p.x; wi.bxh = p.y; wi.byl = p.z; wi.byh = p.w;
+            const float ax = fmaxf(-p.x, p.y), ay = fmaxf(-p.z, p.w);
+            wi.Rw = __builtin_amdgcn_sqrtf(fmaf(ax, ax, ay * ay)) * 1.00001f;
+        }
         stage = st;
+        raw = raw_win;
     }
 #ifdef PVVOTE_TRACE_U1
     const uint64_t t_staged = __builtin_amdgcn_s_memrealtime();
 #endif
     uint32_t qn = 0;
     vote_bytes_seg<MODE>(a, recs, band8, uniform(v), uniform(w), uniform(h0), uniform(nh), 0u, (uint32_t)nh, wq, qn,
-                         tsetup, stage, hq);
+                         tsetup, stage, hq, raw, hraw, &wi);
 #ifdef PVVOTE_TRACE_U1
     const uint64_t t_first = __builtin_amdgcn_s_memrealtime();
 #endif
     __builtin_amdgcn_wave_barrier();
-    fix_queued<MODE>(a, wq, qn);
+    fix_queued<MODE>(a, wq, qn, v, w, h0, raw, hraw);
 #ifdef PVVOTE_TRACE_U1
     if (g_btrace && lane_id() == 0) {
         g_btrace[wave * 8] = t_start;
@@ -2080,6 +2171,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         g_btrace[wave * 8 + 2] = __builtin_amdgcn_s_memrealtime();
         g_btrace[wave * 8 + 3] = t_setup;
         g_btrace[wave * 8 + 4] = t_staged;
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        g_btrace[wave * 8 + 5] = ((uint64_t)xcc << 32) | hw;
     }
 #endif
 }
@@ -2402,15 +2497,19 @@ int pv_voting_for_hypothesis(const float *direct, const float *coords, const flo
     const int64_t items = (int64_t)vn * ba.nwin * ba.nhg;
     if (items >= (1ll << 31)) return PV_EINVAL;   // the kernel's 32-bit item index
     // one launch, no scratch: the operands are made where the blocks stage them
-    unsigned grid = (unsigned)((items + 3) / 4);
+    int wpb = 4;                                  // waves per block
+    if (const char *e5 = getenv("PVVOTE_BYTES_WPB")) wpb = atoi(e5) == 1 ? 1 : 4;
+    unsigned grid = (unsigned)((items + wpb - 1) / wpb);
     ba.xcd = 1;
     if (const char *e4 = getenv("PVVOTE_BYTES_XCD")) ba.xcd = atoi(e4);
     if (ba.xcd) grid = (grid + 7) / 8 * 8;
     hipStream_t s = (hipStream_t)stream;
     if (mode == PV_VOTE_DENSE)
-        k_vote_bytes<PV_VOTE_DENSE><<<grid, 256, 0, s>>>(ba);
+        wpb == 4 ? k_vote_bytes<PV_VOTE_DENSE, 4><<<grid, 256, 0, s>>>(ba)
+                 : k_vote_bytes<PV_VOTE_DENSE, 1><<<grid, 64, 0, s>>>(ba);
     else
-        k_vote_bytes<PV_VOTE_OR><<<grid, 256, 0, s>>>(ba);
+        wpb == 4 ? k_vote_bytes<PV_VOTE_OR, 4><<<grid, 256, 0, s>>>(ba)
+                 : k_vote_bytes<PV_VOTE_OR, 1><<<grid, 64, 0, s>>>(ba);
     return last();
 }
 

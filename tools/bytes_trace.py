@@ -51,3 +51,24 @@ for k in order:
     wv = idx[k]
     g, rest = wv % nhg, wv // nhg
     print(f"wave {wv}: v={rest % VN} w={(rest // VN + nwin - 1) % nwin} g={g}  setup {(su[k] - s[k]) / 100:.2f} loop_end {(f1[k] - s[k]) / 100:.2f} end {(e[k] - t0) / 100:.2f}")
+# per-XCC / per-CU: does a CU's or an XCD's share of waves set its end time?
+hw = t[:, 5]
+xcc = (hw >> 32) & 0xF
+cu = (hw >> 8) & 0xF
+se = (hw >> 13) & 0x7
+cuid = xcc * 64 + se * 16 + cu
+end = (e - t0) / 100
+print("end by XCC (n, median, p90, max):",
+      [f"{k}: {(xcc == k).sum()} {np.median(end[xcc == k]):.2f} {np.percentile(end[xcc == k], 90):.2f} {end[xcc == k].max():.2f}"
+       for k in range(8) if (xcc == k).any()])
+ids, cnt = np.unique(cuid, return_counts=True)
+print("waves per CU histogram:", dict(zip(*np.unique(cnt, return_counts=True))))
+wpc = dict(zip(ids, cnt))
+n_of = np.array([wpc[c] for c in cuid])
+for n in sorted(set(n_of.tolist())):
+    sel = n_of == n
+    print(f"CUs with {n} waves: end median {np.median(end[sel]):.2f} p90 {np.percentile(end[sel], 90):.2f} max {end[sel].max():.2f}")
+# per CU: last end vs first start
+cu_end = {c: end[cuid == c].max() for c in ids}
+v = np.array(list(cu_end.values()))
+print("CU last-end percentiles:", np.round(np.percentile(v, [0, 10, 50, 90, 100]), 2).tolist())
