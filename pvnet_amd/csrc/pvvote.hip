@@ -949,7 +949,9 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
                 for (int i = 0; i < kHypLane; ++i) hit |= m[i] <= gd[i];
                 if (__builtin_amdgcn_ballot_w64(hit)) {
                     ++nfix;
+#ifndef PVVOTE_ABLATE_FIX   // (profiling ablation: band pairs keep the sign count's guess)
                     fix_step(j);
+#endif
                 }
             };
             // the slab past np holds never-voting pixels (negative z, never in
