@@ -942,7 +942,8 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
                 for (int i = 0; i < kHypLane; ++i) {
                     const uint32_t p01 = __builtin_amdgcn_perm(__float_as_uint(z[1][i]), __float_as_uint(z[0][i]), 0x0c0c0b09u);
                     const uint32_t p23 = __builtin_amdgcn_perm(__float_as_uint(z[3][i]), __float_as_uint(z[2][i]), 0x0b090c0cu);
-                    neg[i] = __builtin_amdgcn_sad_u8(p01 | p23, 0u, neg[i]);
+                    // p01 and p23 have no byte in common: sum |p01 - p23| = sum of both
+                    neg[i] = __builtin_amdgcn_sad_u8(p01, p23, neg[i]);
                 }
                 bool hit = false;
 #pragma unroll
@@ -1820,11 +1821,11 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint
     // inlier bytes from the signs of nz = -z: v_perm's selectors 9 / 11
     // replicate the sign bit of its second / first operand into a byte, 12 is 0
     constexpr uint32_t kSgn01 = 0x0c0c0b09u;   // sign(z0) -> b0, sign(z1) -> b1
-    constexpr uint32_t kSel23 = 0x05040100u;   // p01.b0,b1 -> b0,b1; p23.b0,b1 -> b2,b3
+    constexpr uint32_t kSgn23 = 0x0b090c0cu;   // sign(z2) -> b2, sign(z3) -> b3
     auto pack4 = [&](float z0, float z1, float z2, float z3) {
         const uint32_t p01 = __builtin_amdgcn_perm(__float_as_uint(z1), __float_as_uint(z0), kSgn01);
-        const uint32_t p23 = __builtin_amdgcn_perm(__float_as_uint(z3), __float_as_uint(z2), kSgn01);
-        return __builtin_amdgcn_perm(p23, p01, kSel23) & 0x01010101u;   // 1 where z > 0 (band pairs fixed below)
+        const uint32_t p23 = __builtin_amdgcn_perm(__float_as_uint(z3), __float_as_uint(z2), kSgn23);
+        return (p01 | p23) & 0x01010101u;   // 1 where z > 0 (band pairs fixed below); one v_bitop3
     };
     // nz = -z = x' (-tau) + |y'|, and min |nz| for the band check
     auto zrow = [&](const F4 &rec, float nz[kBytePix]) {
