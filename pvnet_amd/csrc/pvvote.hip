@@ -1607,6 +1607,9 @@ struct ByteArgs {
     float thr, tau, gzf, gzr;
     int dbg;               // profiling ablation (PVVOTE_DEBUG_BYTES), 0 = normal
     int xcd;               // XCD-contiguous item ranges (grid a multiple of 8)
+    // CU-balanced grid (bal_nt > 0): bal_t full blocks, then bal_nt quarter
+    // blocks; per XCD bal_tnx / bal_ttx of each (see k_vote_bytes)
+    int bal_t, bal_nt, bal_tnx, bal_ttx;
 };
 
 // Operands of pixel (t, v) in the byte-output kernel, made where they are
@@ -2054,14 +2057,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5, 8))
     // in its setup would otherwise wait for them -- and then finish last
     __builtin_amdgcn_s_setprio(3);
     int blk = (int)blockIdx.x;
-    if (a.xcd) {
-        // blocks i, i + 8, ... run on one XCD (round-robin dispatch; speed
-        // only, nothing depends on it): give each XCD a contiguous range of
-        // items, whose windows' pixels its L2 then fetches once
-        const int per = (int)gridDim.x / 8;   // (the host pads the grid to a multiple of 8)
-        blk = (blk % 8) * per + blk / 8;
-    }
-    const int wave = uniform(blk * WPB + (int)(threadIdx.x / 64));
 #ifdef PVVOTE_TRACE_U1
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     uint64_t t_setup = 0;
@@ -2069,22 +2064,62 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5, 8))
 #else
     uint64_t *tsetup = nullptr;
 #endif
-    const uint32_t nitems = (uint32_t)a.vn * a.nwin * a.nhg;   // < 2^31 (host-checked)
-    // Every load of the wave is issued here, in one round trip at the
-    // launch's start: the item's hypotheses, and the window's pixels.  With
-    // the hypothesis groups in fours (hn a multiple of 256) a block's four
-    // items share (v, w): the block stages the window's pixels in LDS once
-    // (the band-mask area, free until the hot loop) instead of four times.
-    // (nitems is then a multiple of 4: every wave has an item)
+    // Every load of the wave is issued at the launch's start, in one round
+    // trip: the item's hypotheses, and the window's pixels.  With the
+    // hypothesis groups in fours (hn a multiple of 256) a block's four items
+    // share (v, w): the block stages the window's pixels in LDS once (the
+    // band-mask area, free until the hot loop) instead of four times.
     const bool shared = WPB == 4 && a.nhg % 4 == 0;
-    if ((uint32_t)wave >= nitems) return;   // (shared: whole blocks)
-    // items (w, v, g), g fastest: a window's items are adjacent; the last
-    // (partial) window first, so that its slower byte-store rows are not the
-    // launch's tail
-    const uint32_t g = (uint32_t)wave % a.nhg, rest = (uint32_t)wave / a.nhg;
-    const int v = (int)(rest % (uint32_t)a.vn);
-    const int w = (int)((rest / (uint32_t)a.vn + (uint32_t)a.nwin - 1) % (uint32_t)a.nwin);
-    const int h0 = (int)g * kByteHB, nh = min(kByteHB, a.hn - h0);
+    int wave, v, w, h0, nh;
+    if (WPB == 4 && a.bal_nt > 0) {
+        // CU-balanced grid (shared staging only): the bal_t full blocks (64
+        // rows per wave) are a multiple of the CU count; the remaining units
+        // are split four ways into quarter blocks (16 rows per wave),
+        // dispatched after the full ones -- at most one beside a CU's full
+        // blocks, so every CU carries the same rows to within a quarter block
+        // instead of a whole fifth block on some.  Each XCD (blocks i, i + 8,
+        // ... under round-robin dispatch) takes a contiguous share of both
+        // kinds, full ones first.  (Speed only: any placement is correct.)
+        const int x = blk % 8, k = blk / 8;
+        int u, part = -1;
+        if (k < a.bal_tnx) {
+            u = x * a.bal_tnx + k;
+            if (u >= a.bal_t) return;                     // (whole blocks)
+        } else {
+            const int i = x * a.bal_ttx + (k - a.bal_tnx);
+            if (i >= a.bal_nt) return;
+            u = a.bal_t + i / 4;
+            part = i % 4;
+        }
+        const int G = a.nhg / 4, q = (int)(threadIdx.x / 64);
+        const int gq = u % G, rest = u / G;
+        v = rest % a.vn;
+        w = (rest / a.vn + a.nwin - 1) % a.nwin;
+        h0 = part < 0 ? gq * 256 + q * 64 : gq * 256 + part * 64 + q * 16;
+        nh = part < 0 ? kByteHB : 16;
+        wave = uniform(blk * 4 + q);
+    } else {
+        if (a.xcd) {
+            // blocks i, i + 8, ... run on one XCD (round-robin dispatch; speed
+            // only, nothing depends on it): give each XCD a contiguous range of
+            // items, whose windows' pixels its L2 then fetches once
+            const int per = (int)gridDim.x / 8;   // (the host pads the grid to a multiple of 8)
+            blk = (blk % 8) * per + blk / 8;
+        }
+        wave = uniform(blk * WPB + (int)(threadIdx.x / 64));
+        const uint32_t nitems = (uint32_t)a.vn * a.nwin * a.nhg;   // < 2^31 (host-checked)
+        // (shared: nitems is a multiple of 4, every wave of a block has an item)
+        if ((uint32_t)wave >= nitems) return;
+        // items (w, v, g), g fastest: a window's items are adjacent; the last
+        // (partial) window first, so that its slower byte-store rows are not the
+        // launch's tail
+        const uint32_t g = (uint32_t)wave % a.nhg, rest = (uint32_t)wave / a.nhg;
+        v = (int)(rest % (uint32_t)a.vn);
+        w = (int)((rest / (uint32_t)a.vn + (uint32_t)a.nwin - 1) % (uint32_t)a.nwin);
+        h0 = (int)g * kByteHB;
+        nh = min(kByteHB, a.hn - h0);
+    }
+    v = uniform(v); w = uniform(w); h0 = uniform(h0); nh = uniform(nh);
     float2 hq = make_float2(0.f, 0.f);
     if (lane_id() < nh) hq = *(const float2 *)(a.hypo + ((int64_t)(h0 + lane_id()) * a.vn + v) * 2);
     hraw[lane_id()] = hq;
@@ -2506,6 +2541,21 @@ int pv_voting_for_hypothesis(const float *direct, const float *coords, const flo
     ba.xcd = 1;
     if (const char *e4 = getenv("PVVOTE_BYTES_XCD")) ba.xcd = atoi(e4);
     if (ba.xcd) grid = (grid + 7) / 8 * 8;
+    if (wpb == 4 && ba.nhg % 4 == 0 && ba.xcd) {
+        // CU-balanced grid: full blocks a multiple of the CU count, the rest
+        // as quarter blocks, when that leaves at most one quarter block per CU
+        // beside four full ones (one resident round; see k_vote_bytes)
+        const int64_t units = items / 4, cus = cu_count();
+        const int64_t T = units / cus * cus, E = units - T;
+        const char *nb = getenv("PVVOTE_BYTES_NOBAL");
+        if (!(nb && atoi(nb)) && T > 0 && T <= 4 * cus && E > 0 && 4 * E <= cus) {
+            ba.bal_t = (int)T;
+            ba.bal_nt = (int)(4 * E);
+            ba.bal_tnx = (int)((T + 7) / 8);
+            ba.bal_ttx = (int)((4 * E + 7) / 8);
+            grid = (unsigned)(8 * (ba.bal_tnx + ba.bal_ttx));
+        }
+    }
     hipStream_t s = (hipStream_t)stream;
     if (mode == PV_VOTE_DENSE)
         wpb == 4 ? k_vote_bytes<PV_VOTE_DENSE, 4><<<grid, 256, 0, s>>>(ba)

@@ -91,6 +91,26 @@ def test_generate_and_vote_kernels_bit_exact(case, device, rv):
         np.testing.assert_array_equal(out.cpu().numpy().sum(2), g["counts"][0][hs])
 
 
+def test_vote_bytes_full_size(device, rv):
+    """The bench's U1 call (hn=512, tn=29,861: the CU-balanced grid of full
+    and quarter blocks): every row's inliers sum to the golden counts, and
+    sampled rows -- in full blocks and in quarter blocks -- equal the
+    oracle's bytes, in both modes."""
+    g = G.load("synth_v3_512")
+    mask, vertex = G.synth_inputs(g)[:2]
+    coords, direct = O.compact(O.fg_mask_v3(mask[0]), vertex[0])
+    hyp = g["hyp"][0]
+    rows = np.array([0, 63, 64, 200, 255, 256, 300, 447, 448, 460, 497, 511])
+    ref = np.zeros((len(rows), hyp.shape[1], coords.shape[0]), np.uint8)
+    O.voting_for_hypothesis(direct, coords, hyp[rows], ref, 0.99)
+    for dense in (False, True):
+        out = torch.zeros((hyp.shape[0], hyp.shape[1], coords.shape[0]), dtype=torch.uint8, device=device)
+        fn = rv.voting_for_hypothesis_dense if dense else rv.voting_for_hypothesis
+        fn(cu(direct, device), cu(coords, device), cu(hyp, device), out, 0.99)
+        np.testing.assert_array_equal(out.sum(2, dtype=torch.int32).cpu().numpy(), g["counts"][0])
+        np.testing.assert_array_equal(out[torch.from_numpy(rows).to(device)].cpu().numpy(), ref)
+
+
 def test_voting_or_semantics_keeps_existing_bytes(device, rv):
     g = G.load("edge_cases")
     coords, direct = O.compact(O.fg_mask_v3(g["c_mask"][0]), g["c_vertex"][0])
