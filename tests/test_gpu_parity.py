@@ -111,6 +111,27 @@ def test_vote_bytes_full_size(device, rv):
         np.testing.assert_array_equal(out[torch.from_numpy(rows).to(device)].cpu().numpy(), ref)
 
 
+def test_vote_bytes_balanced_grid_other_shape(device, rv):
+    """hn=256, tn=15,000 (270 units on 256 CUs: 256 full + 56 quarter blocks,
+    a different split of the CU-balanced grid): row sums equal the fused
+    vote-count kernel's counts, sampled rows equal the oracle's bytes."""
+    g = G.load("synth_v3_512")
+    mask, vertex = G.synth_inputs(g)[:2]
+    coords, direct = O.compact(O.fg_mask_v3(mask[0]), vertex[0])
+    sel = np.sort(np.random.default_rng(11).choice(coords.shape[0], 15000, replace=False))
+    coords, direct = np.ascontiguousarray(coords[sel]), np.ascontiguousarray(direct[sel])
+    idxs = np.random.default_rng(12).integers(0, 15000, (256, 9, 2)).astype(np.int32)
+    hyp = rv.generate_hypothesis(cu(direct, device), cu(coords, device), cu(idxs, device))
+    cnt = rv.vote_counts(cu(direct, device), cu(coords, device), hyp, 0.99).cpu().numpy()
+    out = torch.empty((256, 9, 15000), dtype=torch.uint8, device=device)
+    rv.voting_for_hypothesis_dense(cu(direct, device), cu(coords, device), hyp, out, 0.99)
+    np.testing.assert_array_equal(out.sum(2, dtype=torch.int32).cpu().numpy(), cnt)
+    rows = np.array([0, 60, 64, 130, 192, 200, 240, 255])
+    ref = np.zeros((len(rows), 9, 15000), np.uint8)
+    O.voting_for_hypothesis(direct, coords, hyp.cpu().numpy()[rows], ref, 0.99)
+    np.testing.assert_array_equal(out[torch.from_numpy(rows).to(device)].cpu().numpy(), ref)
+
+
 def test_voting_or_semantics_keeps_existing_bytes(device, rv):
     g = G.load("edge_cases")
     coords, direct = O.compact(O.fg_mask_v3(g["c_mask"][0]), g["c_vertex"][0])
