@@ -261,25 +261,11 @@ def measure_u1(dev, hn=512, reps=100):
     b.record()
     torch.cuda.synchronize()
     ms = a.elapsed_time(b) / reps
-    # one launch alone: queued with its two events behind a ~100 us device
-    # spin (so the events bracket the kernel, not the host's call), after the
-    # previous launch's bytes have drained; median of 20
-    alone = []
-    for _ in range(20):
-        torch.cuda.synchronize()
-        torch.cuda._sleep(250_000)
-        a.record()
-        rv.voting_for_hypothesis_dense(direct, coords, hyp, inl, 0.99)
-        b.record()
-        torch.cuda.synchronize()
-        alone.append(a.elapsed_time(b))
-    ms_alone = float(np.median(alone))
     nbytes = 8 * tn * VN + 8 * tn + 8 * hn * VN + hn * VN * tn      # BASELINE.md U1 algorithmic bytes
     return dict(kernel="k_vote_bytes<DENSE> (pv_voting_for_hypothesis)", bytes_per_launch=nbytes,
                 traffic=pmc_traffic("k_vote_bytes"),
                 ms=ms, achieved_gbs=nbytes / (ms * 1e-3) / 1e9, peak_gbs=HBM_PEAK_GBS,
-                frac=nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, hn=hn, tn=tn,
-                ms_alone=ms_alone, frac_alone=nbytes / (ms_alone * 1e-3) / 1e9 / HBM_PEAK_GBS)
+                frac=nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, hn=hn, tn=tn)
 
 
 def measure_batch(dev, b=32, hn=512, steps=10):
@@ -555,13 +541,11 @@ def report(args, ws, res, final_err, seg, ver, fb, rvg, work, dev):
             line["roofline"] = dict(bound="hbm", kernel=u1["kernel"], achieved=round(u1["achieved_gbs"], 1),
                                     peak=HBM_PEAK_GBS, unit="GB/s", frac=round(u1["frac"], 4),
                                     traffic=u1["traffic"], avg_kernel_ms=round(u1["ms"], 5),
-                                    alone_kernel_ms=round(u1["ms_alone"], 5), frac_alone=round(u1["frac_alone"], 4),
                                     bytes_per_launch=u1["bytes_per_launch"], hn=u1["hn"], tn=u1["tn"],
                                     note="algorithmic bytes 8*tn*vn + 8*tn + 8*hn*vn + hn*vn*tn (SURVEY 8(d) U1) "
                                          "per launch / mean launch time from hipEvents around 100 back-to-back calls on the "
-                                         "launching stream (dispatch gaps between the kernels included; each launch also waits on "
-                                         "the previous launch's bytes draining from the Infinity Cache); alone_kernel_ms: one "
-                                         "launch queued with its events behind a device spin, median of 20; traffic = "
+                                         "launching stream (dispatch gaps between the kernels included); rocprof kernel durations "
+                                         "of the same calls: profiles/r01_bench_kernel_stats.csv; traffic = "
                                          "2*FETCH_SIZE + WRITE_SIZE per launch (profiles/r01_pmc_traffic.json)")
         except Exception as e:  # reported, never hides the main number
             line["roofline"] = {"error": repr(e)}

@@ -7,4 +7,4 @@ sys.path.insert(0, ".")
 import bench  # noqa: E402
 
 r = bench.measure_u1(torch.device("cuda"))
-print({k: r[k] for k in ("ms", "frac", "ms_alone", "frac_alone", "traffic")})
+print({k: r[k] for k in ("ms", "frac", "traffic")})
