@@ -1582,9 +1582,12 @@ __global__ __launch_bounds__(256) void k_generate_api(const float *direct, const
 // writes their 8 bytes of each row (h, v) at R = (h*vn + v)*tn + t with one
 // 8-byte store, unaligned as the rows are (measured as fast as aligned
 // stores on gfx950).  One item per wave, every item's operand loads at the
-// start of the launch, before the store stream fills the memory system.  A
-// prepass (k_prep_api) lays the pixels out keypoint-major as (ux, uy, cx,
-// cy).  The vote test is vote_segment's rotated-frame test (5 FMAs per
+// start of the launch, before the store stream fills the memory system.
+// There is no prepass: with hn a multiple of 256 a block's four waves take
+// four hypothesis groups of one window and stage the window once (raw
+// operands, fast operands and the window's frame, in LDS); the grid is
+// CU-balanced (full blocks a multiple of the CU count, the rest as quarter
+// blocks).  The vote test is vote_segment's rotated-frame test (5 FMAs per
 // pair); the inlier bytes are the signs of -z gathered with v_perm.  Pairs
 // inside the guard band go to a per-wave LDS queue decided by the
 // reference's sequence at the wave's end; hypotheses / pixels outside the
@@ -2037,8 +2040,9 @@ __device__ __forceinline__ void fix_queued(const ByteArgs &a, const uint16_t *wq
     }
 }
 
-// One item per wave: (keypoint v, window w, hypothesis group g of kByteHB),
-// g fastest; a wave beyond the items exits.
+// One item per wave: (keypoint v, window w, hypothesis group g of kByteHB
+// rows, or of 16 rows in a quarter block of the balanced grid), g fastest;
+// a wave beyond the items exits.
 template <int MODE, int WPB>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_vote_bytes(ByteArgs a) {
     __shared__ F4 recs_all[WPB][kByteHB];
