@@ -1,4 +1,4 @@
-"""World-size-2 stream over gloo on CPU: round-robin sharding and the single
+"""World-size-2 and -4 streams over gloo on CPU: round-robin sharding and the single
 result gather of pvnet_amd.distributed, with the oracle's v3 standing in for
 the device layer (the product path itself needs a GPU)."""
 import os
@@ -56,10 +56,11 @@ def test_shard_round_robin():
         D.shard(4, 2, 2)
 
 
-@pytest.mark.parametrize("n_images", [5, 1])
-def test_stream_world2_gloo(tmp_path, n_images):
+@pytest.mark.parametrize("world, n_images", [(2, 5), (2, 1), (4, 6), (4, 3)])
+def test_stream_gloo(tmp_path, world, n_images):
+    """World sizes 2 and 4 (uneven shards; a rank with no image)."""
     out = str(tmp_path / "res.npy")
-    mp.spawn(_worker, args=(2, _free_port(), n_images, out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), n_images, out), nprocs=world, join=True)
     got = np.load(out)
     want = np.stack([_oracle_vote(*_field(i)).numpy().reshape(3, 2) for i in range(n_images)])
     np.testing.assert_array_equal(got, want)
