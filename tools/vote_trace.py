@@ -79,3 +79,20 @@ print("per-SIMD last end: p10 %.2f p50 %.2f p90 %.2f max %.2f" % (*np.percentile
 print("per-SIMD first end: p10 %.2f p50 %.2f p90 %.2f" % tuple(np.percentile(first_end, [10, 50, 90])))
 gap = last_end - first_end
 print("per-SIMD last-first gap: p10 %.2f p50 %.2f p90 %.2f max %.2f" % (*np.percentile(gap, [10, 50, 90]), gap.max()))
+# Within each SIMD: is a wave's end set by its start order (age-ordered
+# issue), by its hardware wave slot, or by its block's place in the grid?
+uniq, inv = np.unique(wid_in, return_inverse=True)
+srank = np.zeros(len(t), int)
+for g in range(len(uniq)):
+    idx = np.nonzero(inv == g)[0]
+    srank[idx[np.argsort(s_us[idx], kind="stable")]] = np.arange(len(idx))
+erel = e_us - np.array([e_us[inv == inv[i]].min() for i in range(len(t))])
+print("end after the SIMD's first end, by start rank:",
+      [f"{k}: {erel[srank == k].mean():.2f}" for k in range(srank.max() + 1)])
+slot = hw & 0xF
+print("end after the SIMD's first end, by wave slot:",
+      [f"{k}: {erel[slot == k].mean():.2f}" for k in np.unique(slot)])
+blk = np.nonzero(buf.view(-1, 8).cpu().numpy()[:, 0] > 0)[0] // 4
+q = np.digitize(blk, np.percentile(blk, [25, 50, 75]))
+print("end by block-index quartile (mean):", [f"{k}: {e_us[q == k].mean():.2f}" for k in range(4)])
+print("corr(end - SIMD first end, fix steps):", np.corrcoef(erel, nfix)[0, 1])
