@@ -72,3 +72,7 @@ for n in sorted(set(n_of.tolist())):
 cu_end = {c: end[cuid == c].max() for c in ids}
 v = np.array(list(cu_end.values()))
 print("CU last-end percentiles:", np.round(np.percentile(v, [0, 10, 50, 90, 100]), 2).tolist())
+# age: end by block-index quartile (blocks dispatch in index order)
+bidx = idx // 4
+qq = np.digitize(bidx, np.percentile(bidx, [25, 50, 75]))
+print("end by block-index quartile (mean):", [f"{k}: {((e - t0) / 100)[qq == k].mean():.2f}" for k in range(4)])
