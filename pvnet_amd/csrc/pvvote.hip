@@ -2377,8 +2377,9 @@ void launch_vote(const VoteArgs &va, int64_t pixel_steps, hipStream_t s) {
         if (grid == 4 * cu_count()) {
             // four resident rounds: weight the earlier-dispatched ones (round_share;
             // measured: the rounds' mean ends 28.1/30.6/32.9/35.3 us with equal
-            // shares, within ~2 us with these, vote kernel -5 %)
-            int w[4] = {1080, 1024, 976, 920};
+            // shares, within ~2 us with 1080/1024/976/920, vote kernel -6 %;
+            // these a further -1.5 %)
+            int w[4] = {1110, 1035, 965, 890};
             if (const char *e = getenv("PVVOTE_VC_RW")) sscanf(e, "%d,%d,%d,%d", &w[0], &w[1], &w[2], &w[3]);
             for (int k = 0; k < 4; ++k) vr.rw[k] = w[k] > 0 ? w[k] : 1;
         }
