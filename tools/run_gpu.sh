@@ -31,6 +31,8 @@ for s in "$@"; do
     profu1v) for v in ${VARIANTS:-u1base u1nostore u1nocomp}; do PVVOTE_LIB=variants/$v.so step profu1_$v 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$PWD/gpurun_out/profu1_$v" -o u1 -- python3 tools/u1_probe.py; done ;;
     profu1x) PVVOTE_DEBUG_BYTES=3 step profu1x 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$PWD/gpurun_out/profu1x" -o u1 -- python3 tools/u1_probe.py ;;
     profu1) step profu1 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$PWD/gpurun_out/profu1" -o u1 -- python3 tools/u1_probe.py ;;
+    profdriver) step profdriver 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$PWD/gpurun_out/profdriver" -o bench -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    benchdriver) step benchdriver 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     listpmc) step listpmc 300 rocprofv3 -L ;;
     pmcvote) step pmcvote1 600 rocprofv3 --kernel-include-regex k_vote_count --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_INST_CYCLES_SALU -T --output-format csv -d "$PWD/gpurun_out/pmc_vote1" -o v -- python3 bench.py --skip-cpu --skip-e2e --skip-u1 --steps 10 &&
              step pmcvote2 600 rocprofv3 --kernel-include-regex k_vote_count --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_WAVES SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE SQ_INSTS_VALU_TRANS_F32 -T --output-format csv -d "$PWD/gpurun_out/pmc_vote2" -o v -- python3 bench.py --skip-cpu --skip-e2e --skip-u1 --steps 10 &&
