@@ -26,6 +26,7 @@
 //     stores (lane = 8 pixels, hypotheses broadcast from LDS).
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
+#include <array>
 
 #include <algorithm>
 #include <type_traits>
@@ -670,19 +671,19 @@ struct QuarterBoxes {
 // quarter boxes come through LDS.
 template <bool PREPPED, bool SH>
 __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED> *slabs, QuarterBoxes *qbs, int &buf, int b, int v, int hg,
-                                             int ts, int te, int n, int64_t rem_after, int64_t wave_total, int &nfix,
+                                             int ts, int te, int n, uint32_t rem_after, uint32_t prio_hi, uint32_t prio_mid, int &nfix,
                                              uint64_t &tloop) {
     const int lane = lane_id();
     const int wid = SH ? (int)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave) : 0;
     // Issue priority from the work this wave still has (0..3): the SIMD's
     // arbiter otherwise favours the oldest wave, so equal shares finish
     // staggered and the last waves run alone; this keeps them level.
-    // (q = 4 * remaining / (wave_total + 1), compared instead of divided)
-    // (levels 0..2: 3 is the prologue's, above every hot loop)
-    auto set_prio = [&](int64_t remaining) {
-        const int64_t r3 = remaining * 3, w1 = wave_total + 1;
-        if (r3 >= 2 * w1) __builtin_amdgcn_s_setprio(2);
-        else if (r3 >= w1) __builtin_amdgcn_s_setprio(1);
+    // (levels 0..2: 3 is the prologue's, above every hot loop; the caller's
+    // thresholds are ceil(2 (total + 1) / 3) and ceil((total + 1) / 3), so
+    // the comparisons need no 64-bit products: 32-bit, wave-uniform)
+    auto set_prio = [&](uint32_t remaining) {
+        if (remaining >= prio_hi) __builtin_amdgcn_s_setprio(2);
+        else if (remaining >= prio_mid) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
     };
     const float tau = a.tau;
@@ -800,7 +801,6 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const float4 Q = QB.box[k];
-                if (lane == k) { qxl = Q.x; qxh = Q.y; qyl = Q.z; qyh = Q.w; }
                 cxl = fminf(cxl, Q.x); cxh = fmaxf(cxh, Q.y);
                 cyl = fminf(cyl, Q.z); cyh = fmaxf(cyh, Q.w);
                 ex |= QB.exo[k];
@@ -889,8 +889,14 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
         }
         // band of quarter k
         auto set_band = [&](int k) {
-            const float xn = bcast(qxl, k) - ox, xx = bcast(qxh, k) - ox;
-            const float yn = bcast(qyl, k) - oy, yx = bcast(qyh, k) - oy;
+            float xn, xx, yn, yx;
+            if (SH) {   // the block's quarter boxes are still in LDS: no registers held across the loop
+                const float4 Q = QB.box[k];
+                xn = Q.x - ox; xx = Q.y - ox; yn = Q.z - oy; yx = Q.w - oy;
+            } else {
+                xn = bcast(qxl, k) - ox; xx = bcast(qxh, k) - ox;
+                yn = bcast(qyl, k) - oy; yx = bcast(qyh, k) - oy;
+            }
 #pragma unroll
             for (int i = 0; i < kHypLane; ++i) {
                 const float ax = fmaxf(fabsf(hx[i] - xn), fabsf(hx[i] - xx));
@@ -944,6 +950,7 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
             uint32_t neg[kHypLane];
 #pragma unroll
             for (int i = 0; i < kHypLane; ++i) neg[i] = 0;
+            uint64_t hitmask = 0;    // steps (4 pixels each) with a pair in the band
             auto step = [&](F4 q0, F4 q1, F4 q2, F4 q3, int j) {
                 float m[kHypLane];
 #pragma unroll
@@ -965,15 +972,14 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
                     // p01 and p23 have no byte in common: sum |p01 - p23| = sum of both
                     neg[i] = __builtin_amdgcn_sad_u8(p01, p23, neg[i]);
                 }
-                bool hit = false;
+                // (one ballot per compare: the compare's VCC is the ballot)
+                uint64_t hit = 0;
 #pragma unroll
-                for (int i = 0; i < kHypLane; ++i) hit |= m[i] <= gd[i];
-                if (__builtin_amdgcn_ballot_w64(hit)) {
-                    ++nfix;
-#ifndef PVVOTE_ABLATE_FIX   // (profiling ablation: band pairs keep the sign count's guess)
-                    fix_step(j);
-#endif
-                }
+                for (int i = 0; i < kHypLane; ++i) hit |= __builtin_amdgcn_ballot_w64(m[i] <= gd[i]);
+                // a step with a pair in the band is only noted here (bit j / 4 of
+                // a wave-uniform mask) and re-decided after the loop: the exact
+                // sequence's registers are then not live beside the hot loop's
+                if (hit) hitmask |= 1ull << (j >> 2);
             };
             // the slab past np holds never-voting pixels (negative z, never in
             // the band), so the loop runs whole 8-pixel iterations
@@ -988,13 +994,28 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
                 const int j = it * 8;
                 if ((j & (kWave - 1)) == 0) {
                     set_band(j / kWave);
-                    set_prio(rem_after + (te - s0 - j));
+                    set_prio(rem_after + (uint32_t)(te - s0 - j));
                 }
                 const F4 b0 = stage[j + 4], b1 = stage[j + 5], b2 = stage[j + 6], b3 = stage[j + 7];
                 step(a0, a1, a2, a3, j);
                 const int jn = (j + 8) & (kVoteChunk - 1);
                 a0 = stage[jn]; a1 = stage[jn + 1]; a2 = stage[jn + 2]; a3 = stage[jn + 3];
                 step(b0, b1, b2, b3, j + 4);
+            }
+            // the band pairs, by the reference's sequence, under the band of
+            // their own quarter (set_band is deterministic: the same gd as in the loop)
+            {
+                uint64_t hm = hitmask;
+                int kq = -1;
+                while (hm) {
+                    const int j = __builtin_ctzll(hm) * 4;
+                    hm &= hm - 1;
+                    if ((j >> 6) != kq) { kq = j >> 6; set_band(kq); }
+                    ++nfix;
+#ifndef PVVOTE_ABLATE_FIX   // (profiling ablation: band pairs keep the sign count's guess)
+                    fix_step(j);
+#endif
+                }
             }
             // positives = pairs stepped - negatives (never-voting pixels and the
             // padding are negative); hypotheses outside the fast test count 0 here
@@ -1077,7 +1098,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         round_share(total, (uint32_t)nunits, (uint32_t)unit, a.rw, &lo, &hi);
     else
         even_share(total, (uint32_t)nunits, (uint32_t)unit, &lo, &hi);
-    const int64_t wave_total = hi - lo;
+    // issue-priority thresholds of the wave's share (vote_segment set_prio)
+    const uint32_t w1 = hi - lo + 1u;
+    const uint32_t prio_hi = uniform((int)((2ull * w1 + 2) / 3)), prio_mid = uniform((int)((w1 + 2) / 3));
     int nfix = 0, nseg = 0;   // diagnostics (trace)
     uint64_t tloop = 0;       // (trace) first hot-loop entry
     // walk the segments of [lo, hi)
@@ -1094,7 +1117,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         const int v = g / ggn, gg = g - v * ggn;
         const int hg = SH ? gg * 4 + (int)__builtin_amdgcn_readfirstlane(threadIdx.x / 64) : gg;
         vote_segment<PREPPED, SH>(a, slabs, qb_all, buf, uniform(b), uniform(v), uniform(hg), uniform(ts), uniform(te), n,
-                                       (int64_t)(hi - lo) - (te - ts), wave_total, nfix, tloop);
+                                       uniform((int)((hi - lo) - (uint32_t)(te - ts))), prio_hi, prio_mid, nfix, tloop);
         lo += te - ts;
         ++nseg;
     }
@@ -2366,6 +2389,23 @@ int vote_grid_steps(int64_t pixel_steps, const void *kernel, int max_per_cu = 1 
 
 uint64_t *g_vote_trace = nullptr;   // debug hook (pv_debug_set_vote_trace)
 
+// A/B and debug knobs of pv_voting_for_hypothesis, read from the environment
+// once per process (never per call, so graph captures and eager calls agree)
+struct ByteKnobs {
+    int dbg = 0, wpb = 4, xcd = 1, nobal = 0;
+};
+const ByteKnobs &byte_knobs() {
+    static const ByteKnobs k = [] {
+        ByteKnobs r;
+        if (const char *e = getenv("PVVOTE_DEBUG_BYTES")) r.dbg = atoi(e);
+        if (const char *e = getenv("PVVOTE_BYTES_WPB")) r.wpb = atoi(e) == 1 ? 1 : 4;
+        if (const char *e = getenv("PVVOTE_BYTES_XCD")) r.xcd = atoi(e);
+        if (const char *e = getenv("PVVOTE_BYTES_NOBAL")) r.nobal = atoi(e);
+        return r;
+    }();
+    return k;
+}
+
 // the vote launch: block-shared staging when the groups come in fours
 // (SH: at most 4 of its 5 resident blocks per CU, which measured faster for
 // one launch and leaves room for a concurrent image's small kernels)
@@ -2379,8 +2419,13 @@ void launch_vote(const VoteArgs &va, int64_t pixel_steps, hipStream_t s) {
             // measured: the rounds' mean ends 28.1/30.6/32.9/35.3 us with equal
             // shares, within ~2 us with 1080/1024/976/920, vote kernel -6 %;
             // these a further -1.5 %)
-            int w[4] = {1110, 1035, 965, 890};
-            if (const char *e = getenv("PVVOTE_VC_RW")) sscanf(e, "%d,%d,%d,%d", &w[0], &w[1], &w[2], &w[3]);
+            // (PVVOTE_VC_RW overrides them for A/B runs; read once per process,
+            // so every launch -- and every graph capture -- sees the same weights)
+            static const std::array<int, 4> w = [] {
+                std::array<int, 4> r{1110, 1035, 965, 890};
+                if (const char *e = getenv("PVVOTE_VC_RW")) sscanf(e, "%d,%d,%d,%d", &r[0], &r[1], &r[2], &r[3]);
+                return r;
+            }();
             for (int k = 0; k < 4; ++k) vr.rw[k] = w[k] > 0 ? w[k] : 1;
         }
         k_vote_count<PREPPED, true><<<grid, 256, 0, s>>>(vr);
@@ -2568,15 +2613,14 @@ int pv_voting_for_hypothesis(const float *direct, const float *coords, const flo
     ba.fast = fc.fast; ba.thr = fc.thr; ba.tau = fc.tau; ba.gzf = fc.gzf; ba.gzr = fc.gzr;
     ba.nwin = (tn + kByteWin - 1) / kByteWin;
     ba.nhg = (hn + kByteHB - 1) / kByteHB;
-    if (const char *e3 = getenv("PVVOTE_DEBUG_BYTES")) ba.dbg = atoi(e3);
+    const ByteKnobs &kn = byte_knobs();
+    ba.dbg = kn.dbg;
     const int64_t items = (int64_t)vn * ba.nwin * ba.nhg;
     if (items >= (1ll << 31)) return PV_EINVAL;   // the kernel's 32-bit item index
     // one launch, no scratch: the operands are made where the blocks stage them
-    int wpb = 4;                                  // waves per block
-    if (const char *e5 = getenv("PVVOTE_BYTES_WPB")) wpb = atoi(e5) == 1 ? 1 : 4;
+    const int wpb = kn.wpb;                       // waves per block
     unsigned grid = (unsigned)((items + wpb - 1) / wpb);
-    ba.xcd = 1;
-    if (const char *e4 = getenv("PVVOTE_BYTES_XCD")) ba.xcd = atoi(e4);
+    ba.xcd = kn.xcd;
     if (ba.xcd) grid = (grid + 7) / 8 * 8;
     if (wpb == 4 && ba.nhg % 4 == 0 && ba.xcd) {
         // CU-balanced grid: full blocks a multiple of the CU count, the rest
@@ -2584,8 +2628,7 @@ int pv_voting_for_hypothesis(const float *direct, const float *coords, const flo
         // beside four full ones (one resident round; see k_vote_bytes)
         const int64_t units = items / 4, cus = cu_count();
         const int64_t T = units / cus * cus, E = units - T;
-        const char *nb = getenv("PVVOTE_BYTES_NOBAL");
-        if (!(nb && atoi(nb)) && T > 0 && T <= 4 * cus && E > 0 && 4 * E <= cus) {
+        if (!kn.nobal && T > 0 && T <= 4 * cus && E > 0 && 4 * E <= cus) {
             ba.bal_t = (int)T;
             ba.bal_nt = (int)(4 * E);
             ba.bal_tnx = (int)((T + 7) / 8);
