@@ -1,14 +1,17 @@
 """Benchmark: images/sec of PVNet's vote -> keypoint hot path on MI355X.
 
-One step = one batch of synthetic 480x640, 9-keypoint fields (generator S(seed),
-~30k foreground pixels) already resident in HBM, pushed
-through ``ransac_voting_layer_v3`` in its fused network-layout form
-(seg_pred argmax + compaction + 512 hypotheses/keypoint + vote/count + LS
-refine), captured as a hipGraph.  Multi-GPU: one process per GPU, images
-sharded round-robin (weak scaling), one RCCL gather of the keypoints of the
-whole stream to rank 0 at the end of the timed region.
+The stream: synthetic 480x640, 9-keypoint batch-1 frames (generator S(seed),
+~30k foreground pixels), 64 distinct fields per GPU resident
+in HBM and cycled, each pushed through ``ransac_voting_layer_v3`` in its
+fused network-layout form (seg_pred argmax + compaction + 512
+hypotheses/keypoint + vote/count + LS refine).  One step = one replay of a
+hipGraph voting --per-step frames (default 128) with 8 in flight on separate
+streams.  Multi-GPU: one process per GPU, the stream's images sharded
+round-robin (pvnet_amd.distributed.shard: weak scaling), one RCCL all_gather
+of every image's keypoints in stream order (gather_results) at the end of
+the timed region.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--per-step M]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
@@ -35,12 +38,16 @@ FP32_VECTOR_PEAK_TFLOPS = 157.3
 H, W, VN = 480, 640, 9
 
 
+PMC_FILE = "profiles/r02_pmc_traffic.json"
+STATS_FILE = "profiles/r02_bench_kernel_stats.csv"
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed PMC summary
-    (profiles/r01_pmc_traffic.json: 2*FETCH_SIZE + WRITE_SIZE, collected with
-    tools/pmc_traffic.sh on the same bench command), or None."""
+    (PMC_FILE: 2*FETCH_SIZE + WRITE_SIZE, collected with tools/pmc_traffic.sh
+    on the bench command), or None."""
     try:
-        with open(os.path.join(REPO, "profiles", "r01_pmc_traffic.json")) as f:
+        with open(os.path.join(REPO, PMC_FILE)) as f:
             return json.load(f)["kernels"][kernel]["hbm_bytes"]
     except (OSError, KeyError, ValueError):
         return None
@@ -53,13 +60,17 @@ def log(*a):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=1, help="images per GPU per step (configs[1]: batch=1)")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--per-step", type=int, default=128,
+                    help="images per GPU per step: one step = one replay of a hipGraph that votes this many "
+                         "batch-1 frames (configs[1]), `--inflight` of them at a time on separate streams")
+    ap.add_argument("--fields", type=int, default=64,
+                    help="distinct resident S(seed) fields per GPU the stream cycles through (64 x 24.6 MB: the "
+                         "~5 MB each image reads, x64, exceeds the 256 MiB Infinity Cache, so inputs come from HBM)")
     ap.add_argument("--hn", type=int, default=512, help="round_hyp_num (DEMO:55 / TRAIN:141)")
-    ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--inflight", type=int, default=8,
-                    help="images in flight: consecutive steps alternate over this many HIP streams (own workspaces)")
+                    help="images in flight: consecutive images alternate over this many HIP streams (own workspaces)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--skip-e2e", action="store_true")
@@ -80,88 +91,81 @@ def setup_dist(args):
     return ws, rank, torch.device("cuda", local if ws > 1 else 0)
 
 
-def make_inputs(rank, batch, dev):
+def field_seed(i, ws, nfields):
+    """S(seed) of stream image i: the stream cycles through nfields * ws
+    seeds, so rank i % ws holds exactly nfields of them."""
+    return 1234 + i % (nfields * ws)
+
+
+def make_fields(rank, ws, nfields, dev):
+    """The rank's resident fields (network layout, f32), seed 1234 + rank + ws*f."""
     from pvnet_amd import synth
-    fb = synth.synthetic_batch(batch, seed=1234 + 1000 * rank)
-    seg = torch.from_numpy(fb["seg"]).to(dev)
-    ver = torch.from_numpy(fb["vertex"]).to(dev)
-    return seg, ver, fb
+    segs, vers, kps = [], [], []
+    for f in range(nfields):
+        fd = synth.synthetic_field(1234 + rank + ws * f)
+        segs.append(torch.from_numpy(fd["seg"]).to(dev))
+        vers.append(torch.from_numpy(fd["vertex"]).to(dev))
+        kps.append(fd["keypoints"])
+    return segs, vers, np.stack(kps), int(fd["tn"])
 
 
 def main():
     args = parse()
     ws, rank, dev = setup_dist(args)
+    from pvnet_amd import distributed as D
     from pvnet_amd import ransac_voting_gpu as rvg
 
-    seg, ver, fb = make_inputs(rank, args.batch, dev)
-    B, K = args.batch, args.steps
-    work = rvg.VotingWorkspace()
-    out = torch.zeros((K, B, VN, 2), dtype=torch.float32, device=dev)
-    diag = {}
-    # sanity guard on the first call: recovered keypoints vs the generator's truth
-    # (the noisy field itself limits LS accuracy to ~1-2 px; parity is in tests/)
-    kp0 = rvg.ransac_voting_layer_v3_from_network(seg, ver, args.hn, _workspace=work, _diag=diag, _seed=1)
-    torch.cuda.synchronize()
-    tn = diag["tn"].cpu().numpy()
-    err = float(np.abs(kp0.cpu().numpy() - fb["keypoints"]).max())
-    if err > 5.0 and not os.environ.get("PVVOTE_BENCH_NOCHECK"):   # (ablation builds only)
-        raise SystemExit(f"keypoint error {err} px > 5 on the synthetic field (tn={tn})")
-
-    seeds = [rank * 1_000_003 + 17 * k + 3 for k in range(K)]
+    M, K, NF = args.per_step, args.steps, max(1, args.fields)
+    n_images = ws * K * M                          # the whole stream, sharded round-robin (SURVEY 8(e))
+    mine = D.shard(n_images, rank, ws)             # this rank's images, in stream order
+    assert len(mine) == K * M
+    segs, vers, kps, tn = make_fields(rank, ws, NF, dev)
+    # local image j (stream image mine[j]) votes field j % NF: field_seed(mine[j]) == 1234 + rank + ws * (j % NF)
+    assert all(field_seed(mine[j], ws, NF) == 1234 + rank + ws * (j % NF) for j in range(min(len(mine), 4 * NF)))
+    NL = max(1, args.inflight)
+    lanes = [torch.cuda.Stream(device=dev) for _ in range(NL)]
+    works = [rvg.VotingWorkspace() for _ in range(NL)]
+    out_step = torch.zeros((M, VN, 2), dtype=torch.float32, device=dev)
+    local = torch.zeros((K * M, VN, 2), dtype=torch.float32, device=dev)
     s = torch.cuda.Stream(device=dev)
-    NF = max(1, args.inflight)
-    lanes = [torch.cuda.Stream(device=dev) for _ in range(NF)]
-    works = [work] + [rvg.VotingWorkspace() for _ in range(NF - 1)]
 
-    def step(k):
-        # step k runs on in-flight lane k % NF (its own stream and workspace)
-        with torch.cuda.stream(lanes[k % NF]):
-            return rvg.ransac_voting_layer_v3_from_network(seg, ver, args.hn, _seed=seeds[k],
-                                                           _workspace=works[k % NF], out=out[k])
+    def vote(j, seed):
+        # slot j of a step: lane j % NL (its own stream and workspace), field j % NF
+        with torch.cuda.stream(lanes[j % NL]):
+            rvg.ransac_voting_layer_v3_from_network(segs[j % NF], vers[j % NF], args.hn, _seed=seed,
+                                                   _workspace=works[j % NL], out=out_step[j:j + 1])
 
-    def fork():
+    def step_body(seed0):
         for ln in lanes:
             ln.wait_stream(torch.cuda.current_stream())
-
-    def join():
+        for j in range(M):
+            vote(j, seed0 + 17 * j)
         for ln in lanes:
             torch.cuda.current_stream().wait_stream(ln)
 
-    # warmup (eager; kernels are precompiled, nothing is JIT-compiled)
+    # warmup (eager: every lane's workspace sized, nothing is JIT-compiled)
     with torch.cuda.stream(s):
-        fork()
-        for i in range(args.warmup):
-            step(i % K)
-        join()
+        for w in range(max(1, args.warmup)):
+            step_body(1000 * w + rank * 7_919)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            step_body(3 + rank * 1_000_003)
+    graph.replay()                                 # one untimed replay (graph upload)
     torch.cuda.synchronize()
 
-    graph = None
-    if not args.no_graph:
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.stream(s):
-            with torch.cuda.graph(graph, stream=s):
-                fork()
-                for k in range(K):
-                    step(k)
-                join()
-        graph.replay()        # one untimed replay (graph upload)
-        torch.cuda.synchronize()
-
-    gathered = torch.zeros((ws, K, B, VN, 2), dtype=torch.float32, device=dev) if ws > 1 else None
     if ws > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     with torch.cuda.stream(s):
-        if graph is not None:
+        for k in range(K):
             graph.replay()
-        else:
-            fork()
-            for k in range(K):
-                step(k)
-            join()
-        if ws > 1:
-            dist.all_gather_into_tensor(gathered, out)     # the stream's single keypoint exchange (RCCL)
+            local[k * M:(k + 1) * M].copy_(out_step)
+        # the stream's one exchange: keypoints of every image to every rank, in
+        # stream order (pvnet_amd.distributed: RCCL all_gather over xGMI)
+        allkp = D.gather_results(local, n_images, rank, ws)
     torch.cuda.synchronize()
     if ws > 1:
         dist.barrier()
@@ -171,35 +175,50 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # dominant kernel's duration: hipEvents recorded by the library right
-    # before and after the vote kernel on the stream it is launched on, over
-    # eager replays of the same K steps (events inside a captured graph do not
-    # time the nodes between them)
-    vote_ms = time_vote_kernel(rvg, seg, ver, args.hn, seeds, work, out, s)
-    # per-image latency: the same K steps one after another on one stream
+    # sanity on the timed outputs: every local image against its field's
+    # generating keypoints (the noisy field limits LS accuracy to ~1-2 px;
+    # parity is in tests/), and the gathered stream order
+    lk = local.cpu().numpy()
+    err = float(np.abs(lk - kps[np.arange(K * M) % NF]).max())
+    if ws > 1:
+        mine_t = torch.tensor(mine, device=dev)
+        assert torch.equal(allkp[mine_t], local), "gathered stream order differs from the shard"
+        e = torch.tensor([err], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        err = float(e.item())
+    if err > 5.0 and not os.environ.get("PVVOTE_BENCH_NOCHECK"):   # (ablation builds only)
+        raise SystemExit(f"keypoint error {err} px > 5 on the synthetic fields (tn={tn})")
+
+    # dominant kernels' durations with hipEvents on the streams they run on
+    seeds = [rank * 1_000_003 + 17 * k + 3 for k in range(min(K * 5, 100))]
+    vote_ms = time_vote_kernel(rvg, segs, vers, args.hn, seeds, works[0], out_step, s)
+    # per-image latency: 32 images one after another on one stream (rotating fields)
+    NLAT = 32
     lat = torch.cuda.CUDAGraph()
     with torch.cuda.stream(s):
         with torch.cuda.graph(lat, stream=s):
-            for k in range(K):
-                rvg.ransac_voting_layer_v3_from_network(seg, ver, args.hn, _seed=seeds[k], _workspace=work,
-                                                       out=out[k])
+            for j in range(NLAT):
+                rvg.ransac_voting_layer_v3_from_network(segs[j % NF], vers[j % NF], args.hn, _seed=seeds[j % len(seeds)],
+                                                       _workspace=works[0], out=out_step[j % M:j % M + 1])
     lat.replay()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    t1 = time.perf_counter()
     lat.replay()
     torch.cuda.synchronize()
-    latency_ms = (time.perf_counter() - t0) / K * 1e3
-    res = dict(elapsed=elapsed, vote_ms=vote_ms, tn=tn, latency_ms=latency_ms)
-    # sanity on the timed outputs
-    final_err = float(np.abs(out.cpu().numpy() - fb["keypoints"][None]).max())
+    latency_ms = (time.perf_counter() - t1) / NLAT * 1e3
+    res = dict(elapsed=elapsed, vote_ms=vote_ms, tn=tn, latency_ms=latency_ms, n_images=n_images)
     if rank == 0:
-        report(args, ws, res, final_err, seg, ver, fb, rvg, work, dev)
+        report(args, ws, res, err, dev)
     if ws > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def time_vote_kernel(rvg, seg, ver, hn, seeds, work, out, stream):
+def time_vote_kernel(rvg, segs, vers, hn, seeds, work, out, stream):
+    """k_vote_count's duration per launch: hipEvents the library records right
+    before and after the vote kernel on the stream it is launched on, over
+    eager calls cycling through the resident fields (events inside a captured
+    graph do not time the nodes between them)."""
     from pvnet_amd import _lib
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in seeds]
     with torch.cuda.stream(stream):
@@ -208,7 +227,7 @@ def time_vote_kernel(rvg, seg, ver, hn, seeds, work, out, stream):
             b.record(stream)
         for k, (a, b) in enumerate(ev):
             dd = _lib.V3Diag(ev_vote_begin=a.cuda_event, ev_vote_end=b.cuda_event)
-            _raw_v3(rvg, seg, ver, hn, seeds[k], work, out[k], dd)
+            _raw_v3(rvg, segs[k % len(segs)], vers[k % len(vers)], hn, seeds[k], work, out[k % out.shape[0]], dd)
     torch.cuda.synchronize()
     return np.array([a.elapsed_time(b) for a, b in ev])
 
@@ -232,7 +251,11 @@ def _raw_v3(rvg, seg, ver, hn, seed, work, out, dd):
 
 def measure_u1(dev, hn=512, reps=100):
     """API-faithful voting_for_hypothesis (dense u8 [hn,vn,tn] write) on one
-    S(1234) image: the kernel the north star's HBM roofline names (U1)."""
+    S(1234) image: the kernel the north star's HBM roofline names (U1).
+    Timed two ways on the launching stream: hipEvents around `reps`
+    back-to-back calls (device time per call, dispatch gaps included) and an
+    event pair around each of `reps` calls (per-launch durations, each with
+    its event packets' gaps)."""
     from pvnet_amd import ransac_voting as rv
     from pvnet_amd import synth
     f = synth.synthetic_field(1234)
@@ -245,15 +268,9 @@ def measure_u1(dev, hn=512, reps=100):
     idxs = torch.randint(0, tn, (hn, VN, 2), dtype=torch.int32, device=dev)
     hyp = rv.generate_hypothesis(direct, coords, idxs)
     inl = torch.empty((hn, VN, tn), dtype=torch.uint8, device=dev)
-    rv.voting_for_hypothesis_dense(direct, coords, hyp, inl, 0.99)
-    torch.cuda.synchronize()
-    # back-to-back calls between two events on the launching stream, queued
-    # ahead of the device (the host issues a call in well under the kernel's
-    # time): the device time per call, the dispatch gaps between kernels
-    # included.  (Events between the calls would add their own packets'
-    # gaps; rocprof's kernel durations exclude both.)
-    for _ in range(4):
+    for _ in range(5):
         rv.voting_for_hypothesis_dense(direct, coords, hyp, inl, 0.99)
+    torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     for _ in range(reps):
@@ -261,20 +278,32 @@ def measure_u1(dev, hn=512, reps=100):
     b.record()
     torch.cuda.synchronize()
     ms = a.elapsed_time(b) / reps
-    nbytes = 8 * tn * VN + 8 * tn + 8 * hn * VN + hn * VN * tn      # BASELINE.md U1 algorithmic bytes
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for x, y in ev:
+        x.record()
+        rv.voting_for_hypothesis_dense(direct, coords, hyp, inl, 0.99)
+        y.record()
+    torch.cuda.synchronize()
+    per = np.array([x.elapsed_time(y) for x, y in ev])
+    nbytes = 8 * tn * VN + 8 * tn + 8 * hn * VN + hn * VN * tn      # SURVEY 8(d) U1 algorithmic bytes
     return dict(kernel="k_vote_bytes<DENSE> (pv_voting_for_hypothesis)", bytes_per_launch=nbytes,
-                traffic=pmc_traffic("k_vote_bytes"),
-                ms=ms, achieved_gbs=nbytes / (ms * 1e-3) / 1e9, peak_gbs=HBM_PEAK_GBS,
+                traffic=pmc_traffic("k_vote_bytes"), ms=ms, ms_per_launch_median=float(np.median(per)),
+                achieved_gbs=nbytes / (ms * 1e-3) / 1e9, peak_gbs=HBM_PEAK_GBS,
                 frac=nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, hn=hn, tn=tn)
 
 
-def measure_batch(dev, b=32, hn=512, steps=10):
-    """configs[2]-shaped voting throughput: one call votes a batch of 32
-    fields whose foreground spans ~2k..30k pixels (13 disk radii, cycling),
-    captured as a hipGraph of `steps` calls; voting only (fp32)."""
-    from pvnet_amd import ransac_voting_gpu as rvg
+def config2_fields(b=32):
+    """configs[2]-shaped batch: 32 fields whose foreground spans ~2k..30k
+    pixels (13 disk radii, cycling: 'all 13 objects')."""
     from pvnet_amd import synth
-    fs = [synth.synthetic_field(5000 + i, radius=25.0 + 72.5 * (i % 13) / 12.0) for i in range(b)]
+    return [synth.synthetic_field(5000 + i, radius=25.0 + 72.5 * (i % 13) / 12.0) for i in range(b)]
+
+
+def measure_batch(dev, b=32, hn=512, steps=10):
+    """configs[2]'s voting half on its own: one call votes the batch of 32
+    mixed-size fields (fp32 network layout), hipGraph of `steps` calls."""
+    from pvnet_amd import ransac_voting_gpu as rvg
+    fs = config2_fields(b)
     seg = torch.from_numpy(np.concatenate([f["seg"] for f in fs])).to(dev)
     ver = torch.from_numpy(np.concatenate([f["vertex"] for f in fs])).to(dev)
     work = rvg.VotingWorkspace()
@@ -298,8 +327,8 @@ def measure_batch(dev, b=32, hn=512, steps=10):
     err = float(np.abs(out.cpu().numpy() - np.stack([f["keypoints"] for f in fs])[None]).max())
     return dict(images_per_s=round(b * steps / dt, 1), ms_per_batch=round(dt / steps * 1e3, 4), batch=b,
                 tn_range=[min(f["tn"] for f in fs), max(f["tn"] for f in fs)], max_kp_err_px=round(err, 4),
-                note="error vs the generator's keypoints; the smallest disks (tn~2k) alone limit it to ~29 px, "
-                     "the CPU oracle lands within 0.1 px of the same values (parity: tests/)")
+                note="voting only; error vs the generator's keypoints (the smallest disks, tn~2k, alone limit it "
+                     "to ~29 px; parity: tests/test_gpu_parity.py::test_v3_config2_batch32_mixed)")
 
 
 def measure_pnp(dev, b=1024, reps=10, cpu_images=8):
@@ -410,53 +439,114 @@ def measure_pose(dev, b=32, steps=5):
                 note="synthetic box-keypoint fields (0.05 rad noise, 20% outliers); error vs the generating pose")
 
 
-def measure_e2e(dev, half=False, iters=20):
-    """configs[1] (fp32) / configs[2]'s fp16 backbone: ResNet-18 seg+vector-
-    field forward (PyTorch-ROCm, MIOpen, channels_last) + the HIP v3 layer
-    on one 480x640 image, captured together as one hipGraph; random-init
-    weights (the reference ships none), so the foreground is arbitrary and
-    this times the path, not accuracy."""
+FP16_MFMA_DENSE_TFLOPS = 2500.0      # MI355X dense fp16/bf16 matrix peak (no sparsity)
+FP32_MATRIX_TFLOPS = 157.3           # f32 MFMA = the vector peak (MI355X_MICROARCH.md)
+BACKBONE_GFLOP = 144.9               # ResNet-18 OS8 seg+vertex forward at 480x640
+
+
+def measure_e2e(dev, half=False, batch=1, iters=10, hn=512):
+    """configs[1] (fp32, batch 1) / configs[2] (fp16 backbone, batch 32):
+    the ResNet-18 seg+vector-field forward (PyTorch-ROCm, MIOpen,
+    channels_last) and the HIP v3 layer on the network's own outputs (fp16
+    outputs are voted in fp32: the compaction widens them), captured together
+    as one hipGraph.  The outputs are channels_last, so the [b,h,w,vn,2] view
+    of vertex_pred is contiguous and no copy is made.  Random-init weights
+    (the reference ships none): the foreground is whatever the seeded network
+    predicts, so this times the path, not accuracy.  The backbone alone is
+    timed too (its own graph) for its fraction of the matrix peak."""
     from pvnet_amd import ransac_voting_gpu as rvg
     from pvnet_amd.network import PVNet
     torch.backends.cudnn.benchmark = True      # MIOpen: search the convolution algorithms once
     torch.manual_seed(0)
     dt_ = torch.float16 if half else torch.float32
     net = PVNet(18, 2).to(dev).eval().to(dtype=dt_, memory_format=torch.channels_last)
-    x = torch.randn(1, 3, H, W, device=dev).to(dtype=dt_, memory_format=torch.channels_last)
+    x = torch.randn(batch, 3, H, W, device=dev).to(dtype=dt_, memory_format=torch.channels_last)
     ws = rvg.VotingWorkspace()
-    out = torch.zeros((1, VN, 2), dtype=torch.float32, device=dev)
+    out = torch.zeros((batch, VN, 2), dtype=torch.float32, device=dev)
+    diag = {}
+
+    def backbone():
+        with torch.no_grad():
+            return net(x)
 
     def once():
-        with torch.no_grad():
-            sg, v = net(x)
-        return rvg.ransac_voting_layer_v3_from_network(sg.contiguous(), v.contiguous(), 512, _workspace=ws,
-                                                       max_num=30000, _seed=7, out=out)
-    s = torch.cuda.Stream(device=dev)
-    with torch.cuda.stream(s):
-        for _ in range(3):
-            once()
-    torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.stream(s):
-        with torch.cuda.graph(g, stream=s):
-            once()
-    g.replay()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(iters):
+        sg, v = backbone()
+        return rvg.ransac_voting_layer_v3_from_network(sg, v, hn, _workspace=ws, max_num=30000, _seed=7, out=out)
+
+    def timed(fn):
+        s = torch.cuda.Stream(device=dev)
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                fn()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                fn()
         g.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            g.replay()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / iters
+
+    with torch.no_grad():
+        sg, v = backbone()
+        rvg.ransac_voting_layer_v3_from_network(sg, v, hn, _workspace=ws, _seed=7, _diag=diag)
     torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / iters
-    return dict(images_per_s=round(1.0 / dt, 1), ms_per_image=round(dt * 1e3, 4),
-                backbone_dtype="float16" if half else "float32", backbone_gflop=144.9,
-                backbone_tflops=round(144.9e9 / dt / 1e12, 1),
-                note="random-init weights (none ship with the reference): timing only")
+    tn = diag["tn"].cpu().numpy()
+    dt = timed(once)
+    dtb = timed(backbone)
+    peak = FP16_MFMA_DENSE_TFLOPS if half else FP32_MATRIX_TFLOPS
+    bb_tf = BACKBONE_GFLOP * batch / dtb / 1e3
+    return dict(images_per_s=round(batch / dt, 1), ms_per_batch=round(dt * 1e3, 4), batch=batch,
+                backbone_dtype="float16" if half else "float32", voting_dtype="float32",
+                backbone_ms_per_batch=round(dtb * 1e3, 4), backbone_gflop_per_image=BACKBONE_GFLOP,
+                backbone_tflops=round(bb_tf, 1), backbone_matrix_peak_tflops=peak,
+                backbone_frac_of_matrix_peak=round(bb_tf / peak, 4),
+                voting_ms_per_batch=round((dt - dtb) * 1e3, 4), foreground_px=[int(tn.min()), int(tn.max())],
+                note="random-init weights (none ship with the reference): timing only; images/s covers backbone + "
+                     "v3 in one graph; the backbone alone is a separate graph (MIOpen kernels: "
+                     "profiles/r02_backbone_kernel_stats.csv)")
+
+
+def measure_kp_vs_ref(dev):
+    """The metric's '2D kp L2 err vs ref': the device v3 with the golden
+    fixtures' injected pixel pairs on the fixtures' own inputs (the LINEMOD
+    'cat' demo field and S(1234)), against the keypoints the reference's
+    ransac_voting_gpu.py produced for them (tests/golden/*_v3_512.npz; no
+    oracle involved)."""
+    from pvnet_amd import ransac_voting_gpu as rvg
+    from tests import golden_io as G
+    res = {}
+    for case in ("cat_v3_512", "synth_v3_512"):
+        g = G.load(case)
+        mask, vertex = (G.cat_inputs(g) if case.startswith("cat") else G.synth_inputs(g))[:2]
+        kp = rvg.ransac_voting_layer_v3(torch.from_numpy(mask).to(dev), torch.from_numpy(vertex).to(dev), 512,
+                                        _idxs=g["idxs"]).cpu().numpy()
+        l2 = np.linalg.norm(kp - g["keypoints"], axis=-1)
+        res[case.split("_")[0]] = dict(max_px=float(l2.max()), mean_px=float(l2.mean()))
+    return res
+
+
+def host_cores():
+    """Every host core this process may run on: the affinity mask, bounded by
+    the cgroup CPU quota when one is set (a GPU box's CPU share)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def cpu_baseline(budget_s):
     """The oracle's v3 (C kernels, OpenMP) on the host cores, on a bounded
-    sample of the same workload (S(1234), hn=512): the box's CPU share
-    (16 threads) and one thread, each image timed, median reported."""
+    sample of the same workload (S(1234), hn=512): every core this process
+    may use (host_cores()) and one thread, each image timed, median reported."""
     from oracle import oracle as O
     from pvnet_amd import synth
     f = synth.synthetic_field(1234)
@@ -480,33 +570,34 @@ def cpu_baseline(budget_s):
             O.vote_counts = orig
         return times
 
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_cores()
     tm = run(threads, budget_s * 0.6, 50)
     t1 = run(1, budget_s * 0.4, 5)
     return dict(value=round(1.0 / float(np.median(tm)), 3), unit="images/sec", cores=threads, kind="port",
+                affinity_cpus=len(os.sched_getaffinity(0)),
                 value_1core=round(1.0 / float(np.median(t1)), 4),
                 sample=f"median of {len(tm)} ({threads} threads) / {len(t1)} (1 thread) S(1234) 480x640 fields, "
                        f"tn=29861, hn=512: v3 incl. compaction + refine (oracle/pvvote_oracle.c, OpenMP)")
 
 
-def report(args, ws, res, final_err, seg, ver, fb, rvg, work, dev):
-    K, B = args.steps, args.batch
+def report(args, ws, res, final_err, dev):
+    K, M = args.steps, args.per_step
     elapsed = res["elapsed"]
-    value = ws * K * B / elapsed
+    value = res["n_images"] / elapsed
     tn = res["tn"]
     vote_ms = float(np.mean(res["vote_ms"]))
-    pairs = float(args.hn * VN * tn.sum())          # per launch: one launch votes the whole local batch
+    pairs = float(args.hn * VN * tn)                # per launch: one launch votes one batch-1 frame
     flops = 12.0 * pairs                            # 12 FLOP per (h,v,t)
     achieved = flops / (vote_ms * 1e-3) / 1e12
     vc = dict(bound="valu", kernel="k_vote_count (fused vote+count, U2)", achieved=round(achieved, 2),
-                peak=FP32_VECTOR_PEAK_TFLOPS, unit="TFLOP/s", frac=round(achieved / FP32_VECTOR_PEAK_TFLOPS, 4),
-                traffic=pmc_traffic("k_vote_count"), avg_kernel_ms=round(vote_ms, 5), flop_per_launch=flops,
-                note="12 FLOP per (hypothesis, keypoint, pixel) pair (SURVEY 8(d) U2); no inlier mask is "
-                     "materialised, the compulsory bytes are the pixel operands (32 B per pixel and keypoint, "
-                     "read once per block of four hypothesis groups) and the counts, so the bound is the vector "
-                     "ALU, not HBM or MFMA; traffic = 2*FETCH_SIZE + WRITE_SIZE per launch from "
-                     "profiles/r01_pmc_traffic.json; avg_kernel_ms from hipEvents around eager launches (includes "
-                     "~3 us of launch overhead that rocprof's kernel duration does not)")
+              peak=FP32_VECTOR_PEAK_TFLOPS, unit="TFLOP/s", frac=round(achieved / FP32_VECTOR_PEAK_TFLOPS, 4),
+              traffic=pmc_traffic("k_vote_count"), avg_kernel_ms=round(vote_ms, 5), flop_per_launch=flops,
+              note="12 FLOP per (hypothesis, keypoint, pixel) pair (SURVEY 8(d) U2); no inlier mask is "
+                   "materialised, the compulsory bytes are the pixel operands (32 B per pixel and keypoint) and "
+                   "the counts, so the bound is the vector ALU, not HBM or MFMA; traffic = 2*FETCH_SIZE + "
+                   "WRITE_SIZE per launch (%s); avg_kernel_ms from hipEvents the library records around the "
+                   "kernel on its stream in eager calls (rocprof durations of the same run: %s)"
+                   % (PMC_FILE, STATS_FILE))
     line = {
         "metric": "images/sec (480x640, 9 kp) vote->keypoint",
         "value": round(value, 2),
@@ -520,18 +611,26 @@ def report(args, ws, res, final_err, seg, ver, fb, rvg, work, dev):
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic S(seed) fields (SURVEY 8(d)): disk r=97.5 -> 29,861 fg px, 9 kp, 0.05 rad noise, "
-                "20% outliers; network layout seg_pred/vertex_pred resident in HBM",
-        "config": {"workload": "LINEMOD-cat-sized frame, batch=%d per GPU per step: ransac_voting_layer_v3 "
-                               "(hn=%d, thr=0.99) from seg_pred/vertex_pred, hipGraph of %d steps, %d steps in "
-                               "flight on separate streams" % (B, args.hn, K, max(1, args.inflight)),
-                   "global_batch": B * ws, "image": [H, W], "keypoints": VN, "round_hyp_num": args.hn,
-                   "foreground_px": int(tn[0]), "parallelism": "dp%d (images sharded, RCCL gather)" % ws,
-                   "images_in_flight": max(1, args.inflight)},
+                "20%% outliers; network-layout seg_pred/vertex_pred f32 resident in HBM, %d distinct fields per "
+                "GPU cycled (%.0f MB, beyond the 256 MiB Infinity Cache)" % (args.fields, args.fields * 24.576),
+        "config": {"workload": "stream of LINEMOD-cat-sized batch-1 frames (configs[1]'s voting layer): "
+                               "ransac_voting_layer_v3 (hn=%d, thr=0.99) from seg_pred/vertex_pred; one step = one "
+                               "hipGraph replay voting %d frames per GPU, %d in flight on separate streams; "
+                               "images sharded round-robin over ranks, one gather of all keypoints at the end"
+                               % (args.hn, M, max(1, args.inflight)),
+                   "global_batch": M * ws, "per_gpu_batch_per_step": M, "image": [H, W], "keypoints": VN,
+                   "round_hyp_num": args.hn, "foreground_px": int(tn),
+                   "parallelism": "dp%d (images sharded round-robin, RCCL all_gather of keypoints)" % ws,
+                   "images_in_flight": max(1, args.inflight), "stream_images": res["n_images"]},
         "roofline": None,
         "roofline_vote_count": vc,
         "max_kp_err_px": round(final_err, 5),
         "latency_ms_per_image": round(res["latency_ms"], 5),
     }
+    try:
+        line["kp_err_vs_ref_px"] = measure_kp_vs_ref(dev)
+    except Exception as e:
+        line["kp_err_vs_ref_px"] = {"error": repr(e)}
     # `roofline`: the kernel the north star names, voting_for_hypothesis (U1),
     # against the HBM peak; the pipeline's own dominant kernel (k_vote_count,
     # VALU-bound: no inlier mask is materialised) is `roofline_vote_count`
@@ -541,35 +640,25 @@ def report(args, ws, res, final_err, seg, ver, fb, rvg, work, dev):
             line["roofline"] = dict(bound="hbm", kernel=u1["kernel"], achieved=round(u1["achieved_gbs"], 1),
                                     peak=HBM_PEAK_GBS, unit="GB/s", frac=round(u1["frac"], 4),
                                     traffic=u1["traffic"], avg_kernel_ms=round(u1["ms"], 5),
+                                    per_launch_events_median_ms=round(u1["ms_per_launch_median"], 5),
                                     bytes_per_launch=u1["bytes_per_launch"], hn=u1["hn"], tn=u1["tn"],
                                     note="algorithmic bytes 8*tn*vn + 8*tn + 8*hn*vn + hn*vn*tn (SURVEY 8(d) U1) "
-                                         "per launch / mean launch time from hipEvents around 100 back-to-back calls on the "
-                                         "launching stream (dispatch gaps between the kernels included); rocprof kernel durations "
-                                         "of the same calls: profiles/r01_bench_kernel_stats.csv; traffic = "
-                                         "2*FETCH_SIZE + WRITE_SIZE per launch (profiles/r01_pmc_traffic.json)")
+                                         "per launch / avg_kernel_ms = hipEvents around 100 back-to-back calls on "
+                                         "the launching stream (dispatch gaps included); per-launch event pairs "
+                                         "also reported; rocprof kernel durations of the same command: %s; "
+                                         "traffic = 2*FETCH_SIZE + WRITE_SIZE per launch (%s)" % (STATS_FILE, PMC_FILE))
         except Exception as e:  # reported, never hides the main number
             line["roofline"] = {"error": repr(e)}
     if not args.skip_e2e:
-        try:
-            line["e2e_config1"] = measure_e2e(dev)
-        except Exception as e:
-            line["e2e_config1"] = {"error": repr(e)}
-        try:
-            line["e2e_fp16_backbone"] = measure_e2e(dev, half=True)
-        except Exception as e:
-            line["e2e_fp16_backbone"] = {"error": repr(e)}
-        try:
-            line["voting_config2_batch32"] = measure_batch(dev)
-        except Exception as e:
-            line["voting_config2_batch32"] = {"error": repr(e)}
-        try:
-            line["pnp_config5"] = measure_pnp(dev)
-        except Exception as e:
-            line["pnp_config5"] = {"error": repr(e)}
-        try:
-            line["pose_config5_batch32"] = measure_pose(dev)
-        except Exception as e:
-            line["pose_config5_batch32"] = {"error": repr(e)}
+        for key, fn in (("e2e_config1", lambda: measure_e2e(dev)),
+                        ("e2e_config2_fp16_batch32", lambda: measure_e2e(dev, half=True, batch=32)),
+                        ("voting_config2_batch32", lambda: measure_batch(dev)),
+                        ("pnp_config5", lambda: measure_pnp(dev)),
+                        ("pose_config5_batch32", lambda: measure_pose(dev))):
+            try:
+                line[key] = fn()
+            except Exception as e:
+                line[key] = {"error": repr(e)}
     if ws == 1 and not args.skip_cpu:
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     print(json.dumps(line), flush=True)

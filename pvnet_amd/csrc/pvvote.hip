@@ -2394,8 +2394,8 @@ uint64_t *g_vote_trace = nullptr;   // debug hook (pv_debug_set_vote_trace)
 struct ByteKnobs {
     int dbg = 0, wpb = 4, xcd = 1, nobal = 0;
 };
-const ByteKnobs &byte_knobs() {
-    static const ByteKnobs k = [] {
+ByteKnobs &byte_knobs() {
+    static ByteKnobs k = [] {
         ByteKnobs r;
         if (const char *e = getenv("PVVOTE_DEBUG_BYTES")) r.dbg = atoi(e);
         if (const char *e = getenv("PVVOTE_BYTES_WPB")) r.wpb = atoi(e) == 1 ? 1 : 4;
@@ -2697,6 +2697,12 @@ int pv_debug_wave_minmax(const float *in, float *out, int32_t nwaves, pv_stream_
 
 // debug only (not in pvvote.h): per-wave timestamps of the next pipeline vote launches
 void pv_debug_set_vote_trace(uint64_t *buf) { g_vote_trace = buf; }
+// test hook: the byte kernel's debug mode (PVVOTE_DEBUG_BYTES) at run time; returns the previous one
+int pv_debug_set_bytes_mode(int32_t dbg) {
+    const int prev = byte_knobs().dbg;
+    byte_knobs().dbg = dbg;
+    return prev;
+}
 #ifdef PVVOTE_TRACE_U1
 int pv_debug_set_bytes_trace(uint64_t *buf) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_btrace), &buf, sizeof(buf)); }
 #endif

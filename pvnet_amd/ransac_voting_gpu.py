@@ -53,21 +53,42 @@ def _draw_seed() -> int:
 
 class VotingWorkspace:
     """Device scratch for the pipelines, reused across calls of the same shape
-    (needed for hipGraph capture: no allocation inside the captured region)."""
+    (needed for hipGraph capture: no allocation inside the captured region).
 
-    def __init__(self):
+    A pipeline call zeroes and rewrites its workspace, so two calls in flight
+    on different streams must not share one: an explicit workspace belongs to
+    one stream at a time (pass one per stream, as ``bench.py`` does), and the
+    default workspace (used when ``_workspace`` is omitted) keeps one buffer
+    per (device, stream).  A buffer that grows is released with
+    ``record_stream`` for every stream that used it, so the caching allocator
+    never hands it out while a kernel can still touch it.  Growing inside a
+    graph capture raises: warm the workspace up (one eager call of the same
+    shape) before capturing."""
+
+    def __init__(self, per_stream: bool = False):
         self._buf = {}
+        self._streams = {}
+        self._per_stream = per_stream
 
     def get(self, device, nbytes: int) -> torch.Tensor:
-        key = (str(device),)
+        stream = torch.cuda.current_stream(device)
+        key = (str(device), stream.cuda_stream) if self._per_stream else (str(device),)
         buf = self._buf.get(key)
         if buf is None or buf.numel() < nbytes:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("VotingWorkspace would allocate during graph capture: make one eager call of "
+                                   "the same shape with this workspace (_workspace=...) before capturing")
+            if buf is not None:
+                for st in self._streams.get(key, ()):
+                    buf.record_stream(st)
             buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
             self._buf[key] = buf
+            self._streams[key] = set()
+        self._streams[key].add(stream)
         return buf
 
 
-_default_ws = VotingWorkspace()
+_default_ws = VotingWorkspace(per_stream=True)
 
 
 def _desc(mask, vertex, seg=False):

@@ -6,6 +6,7 @@ import pytest
 import torch
 
 from oracle import oracle as O
+from pvnet_amd import _lib
 from tests import golden_io as G
 
 pytestmark = pytest.mark.gpu
@@ -173,11 +174,18 @@ def test_guard_band_stress(seed, device, rv):
 
 
 @pytest.mark.parametrize("full_queue", [False, True])
-def test_band_pairs_both_modes(full_queue, device, rv, monkeypatch):
+def test_band_pairs_both_modes(full_queue, device, rv):
     """Band pairs go through k_fix_bytes' queue (or, with the queue full, the
     in-kernel exact pass): dense and OR modes, thresholds on reference cosines."""
-    if full_queue:
-        monkeypatch.setenv("PVVOTE_DEBUG_BYTES", "4")
+    L = _lib.load()
+    prev = L.pv_debug_set_bytes_mode(4 if full_queue else 0)    # (test-only export, not in the header)
+    try:
+        _band_pairs_both_modes(device, rv)
+    finally:
+        L.pv_debug_set_bytes_mode(prev)
+
+
+def _band_pairs_both_modes(device, rv):
     rng = np.random.default_rng(7)
     tn, vn, hn = 2500, 2, 96
     coords = np.stack([rng.integers(0, 640, tn), rng.integers(0, 480, tn)], 1).astype(np.float32)
@@ -456,3 +464,72 @@ def test_motion_voting(device, rvg):
     np.testing.assert_allclose(got, g["points"], atol=1e-3, rtol=0)
     np.testing.assert_allclose(got, O.ransac_motion_voting(g["mask"], g["vertex"]), atol=1e-4, rtol=0)
     assert np.all(got[2] == 0)
+
+
+# ---------------------------------------------------------------- configs[2]
+@pytest.mark.parametrize("half", [False, True])
+def test_v3_config2_batch32_mixed(half, device, rvg):
+    """configs[2]'s voting call: one batch of 32 network-layout fields whose
+    foreground spans ~2k..30k pixels (13 disk radii, cycling), hn=512, with
+    injected pixel pairs; fp16 network outputs (the fp16 backbone's) are voted
+    in fp32.  Every image's counts equal the oracle's bit for bit (the oracle
+    votes the same fp16-rounded directions) and its keypoints agree."""
+    from pvnet_amd import synth
+    b, hn = 32, 512
+    fs = [synth.synthetic_field(5000 + i, radius=25.0 + 72.5 * (i % 13) / 12.0) for i in range(b)]
+    dt = np.float16 if half else np.float32
+    seg = np.concatenate([f["seg"] for f in fs]).astype(dt)
+    ver = np.concatenate([f["vertex"] for f in fs]).astype(dt)
+    rng = np.random.default_rng(32)
+    idxs = np.stack([rng.integers(0, f["tn"], (hn, 9, 2)) for f in fs]).astype(np.int32)
+    diag = {}
+    kp = rvg.ransac_voting_layer_v3_from_network(cu(seg, device), cu(ver, device), hn, _idxs=idxs,
+                                                 _diag=diag).cpu().numpy()
+    counts = diag["counts"].cpu().numpy()
+    assert sorted(int(f["tn"]) for f in fs)[0] < 2500 and max(int(f["tn"]) for f in fs) == 29861
+    for i in range(b):
+        vv = np.ascontiguousarray(ver[i:i + 1].astype(np.float32).transpose(0, 2, 3, 1).reshape(1, 480, 640, 9, 2))
+        dg = []
+        ko = O.ransac_voting_layer_v3(np.argmax(seg[i:i + 1].astype(np.float32), 1), vv, hn, idxs=[idxs[i]], diag=dg)
+        np.testing.assert_array_equal(counts[i].T, dg[0]["counts"], err_msg=f"image {i}")
+        np.testing.assert_allclose(kp[i], ko[0], atol=KP_TOL, err_msg=f"image {i}")
+
+
+def test_default_workspace_two_streams(device, rvg):
+    """Calls without _workspace on two streams at once: the default
+    workspace keeps one buffer per (device, stream), so concurrent calls do not
+    overwrite each other's scratch; results equal the sequential ones."""
+    from pvnet_amd import synth
+    fa, fb = synth.synthetic_field(41), synth.synthetic_field(42)
+    ia = np.random.default_rng(1).integers(0, fa["tn"], (1, 256, 9, 2)).astype(np.int32)
+    ib = np.random.default_rng(2).integers(0, fb["tn"], (1, 256, 9, 2)).astype(np.int32)
+    sa, va, sb, vb = (cu(fa["seg"], device), cu(fa["vertex"], device), cu(fb["seg"], device), cu(fb["vertex"], device))
+    ra = rvg.ransac_voting_layer_v3_from_network(sa, va, 256, _idxs=ia).cpu().numpy()
+    rb = rvg.ransac_voting_layer_v3_from_network(sb, vb, 256, _idxs=ib).cpu().numpy()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for _ in range(3):
+        s1.wait_stream(torch.cuda.current_stream())
+        s2.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s1):
+            oa = rvg.ransac_voting_layer_v3_from_network(sa, va, 256, _idxs=ia)
+        with torch.cuda.stream(s2):
+            ob = rvg.ransac_voting_layer_v3_from_network(sb, vb, 256, _idxs=ib)
+        torch.cuda.current_stream().wait_stream(s1)
+        torch.cuda.current_stream().wait_stream(s2)
+        outs.append((oa, ob))
+    torch.cuda.synchronize()
+    for oa, ob in outs:
+        np.testing.assert_array_equal(oa.cpu().numpy(), ra)
+        np.testing.assert_array_equal(ob.cpu().numpy(), rb)
+
+
+def test_workspace_growth_inside_capture_raises(device, rvg):
+    """A workspace that would allocate inside a graph capture raises (warm it up first)."""
+    from pvnet_amd import synth
+    f = synth.synthetic_field(43, H=96, W=128, radius=30.5, center=(64.0, 48.0))
+    seg, ver = cu(f["seg"], device), cu(f["vertex"], device)
+    g = torch.cuda.CUDAGraph()
+    with pytest.raises(RuntimeError, match="graph capture"):
+        with torch.cuda.graph(g):
+            rvg.ransac_voting_layer_v3_from_network(seg, ver, 64, _workspace=rvg.VotingWorkspace(), _seed=1)

@@ -1,0 +1,20 @@
+#!/bin/bash
+# The driver's exact bench command, plain and under rocprofv3 --kernel-trace
+# --stats (the summary behind the JSON line's kernel durations), then one
+# FETCH_SIZE and one WRITE_SIZE pass (tools/pmc_traffic_json.py folds them).
+# Every GPU step under its own time limit; stop at the first failure.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+CMD="bench.py --gpus 1 --steps 20 --warmup 5"
+timeout -k 10 400 python3 $CMD > gpurun_out/bench_plain.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/bench_plain.log; exit 1; }
+grep '^{' gpurun_out/bench_plain.log | tail -1 > gpurun_out/bench_plain.json
+timeout -k 10 500 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$PWD/gpurun_out/prof_bench" -o bench -- python3 $CMD > gpurun_out/bench_prof.log 2>&1 || { echo "prof failed"; tail -20 gpurun_out/bench_prof.log; exit 1; }
+grep '^{' gpurun_out/bench_prof.log | tail -1 > gpurun_out/bench_prof.json
+if [ -n "$PMC" ]; then
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 400 rocprofv3 --kernel-include-regex "k_vote|k_compact|k_fg_count|k_refine|k_hyp_gen|k_front" --pmc $c -T --output-format csv \
+      -d "$PWD/gpurun_out/pmc_$c" -o b -- python3 bench.py --steps 5 --warmup 2 --skip-cpu --skip-e2e > gpurun_out/pmc_$c.log 2>&1 || { echo "pmc $c failed"; exit 1; }
+  done
+  python3 tools/pmc_traffic_json.py gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE gpurun_out/pmc_traffic.json > /dev/null
+fi
+echo ok
