@@ -169,18 +169,15 @@ __device__ __forceinline__ bool is_fg(const MaskView &m, int b, int r, int c) {
 struct Workspace {
     int32_t *counts;    // [b][vn][nh]   zeroed by k_fg_count
     int32_t *ticket;    // [b][1 + vn]   zeroed by k_fg_count: per image, per (image, keypoint)
-    uint32_t *exotic;   // [b][nchv]     zeroed by k_fg_count (chunk holds a pixel outside the fast domain)
     int32_t *dsagg;     // [b][nblk]     zeroed by k_fg_count: downsampled count + 1 per block (look-back)
     int32_t *confc;     // [b][vn][2]    zeroed by k_fg_count: v5 confidence count, ticket
-    int64_t nchv;       // vote chunks per image (capacity)
-    int64_t zero_words; // counts + ticket + exotic + dsagg (contiguous)
+    int64_t zero_words; // counts + ticket + dsagg + confc (contiguous)
     int32_t *tn;        // [b] compacted pixels (0 = image skipped)
     int32_t *fgtot;     // [b] foreground before downsampling
     int32_t *blkcnt;    // [b][nblk]
+    uint64_t *fgbits;   // [b][nblk][4] foreground ballot of each wave of a k_fg_count block
     float4 *pex;        // [b][vn][P]   exact pixel data (cx, cy, nx, ny): reference operands
-    float4 *pix;        // [b][vn][P]   fast-test data (fx, cy, ux, uy)
     float2 *hyp;        // [b][nh][vn]  (reference layout)
-    float2 *hypv;       // [b][vn][nh]  the same, keypoint-major (the vote kernel's coalesced reads)
     int32_t *win;       // [b][vn]
     float *ratio;       // [b][vn]
     double *refpart;    // [b][vn][kRefineNJ][5]
@@ -195,20 +192,17 @@ Workspace carve(void *base, int b, int H, int W, int vn, int nh) {
     char *p = (char *)base;
     int64_t off = 0;
     auto take = [&](int64_t bytes) { char *q = p ? p + off : nullptr; off = align_up(off + bytes, 256); return q; };
-    w.nchv = (P + kVoteChunk - 1) / kVoteChunk;
-    w.zero_words = (int64_t)b * vn * nh + (int64_t)b * (1 + vn) + b * w.nchv + b * nblk + 2 * (int64_t)b * vn;
+    w.zero_words = (int64_t)b * vn * nh + (int64_t)b * (1 + vn) + b * nblk + 2 * (int64_t)b * vn;
     w.counts = (int32_t *)take(4 * w.zero_words);
     w.ticket = w.counts ? w.counts + (int64_t)b * vn * nh : nullptr;
-    w.exotic = w.counts ? (uint32_t *)(w.ticket + (int64_t)b * (1 + vn)) : nullptr;
-    w.dsagg = w.counts ? (int32_t *)(w.exotic + b * w.nchv) : nullptr;
+    w.dsagg = w.counts ? w.ticket + (int64_t)b * (1 + vn) : nullptr;
     w.confc = w.counts ? w.dsagg + b * nblk : nullptr;
     w.tn = (int32_t *)take(4 * b);
     w.fgtot = (int32_t *)take(4 * b);
     w.blkcnt = (int32_t *)take(4 * b * nblk);
+    w.fgbits = (uint64_t *)take(8 * 4 * b * nblk);
     w.pex = (float4 *)take(16 * b * vn * P);
-    w.pix = (float4 *)take(16 * b * vn * P);
     w.hyp = (float2 *)take(8 * (int64_t)b * nh * vn);
-    w.hypv = (float2 *)take(8 * (int64_t)b * nh * vn);
     w.win = (int32_t *)take(4 * b * vn);
     w.ratio = (float *)take(4 * b * vn);
     w.refpart = (double *)take(8 * 5 * (int64_t)b * vn * kRefineNJ);
@@ -245,11 +239,14 @@ __device__ __forceinline__ int2 block_sum2(int x, int y, int *sh) {
 }
 
 // ==========================================================================
-// K1: foreground count per 1024-pixel block; zeroes the pipeline's counters
+// K1: foreground count per 256-pixel block (one pixel per thread) and the
+// block's four wave ballots (k_compact reads 32 B instead of the mask again);
+// zeroes the pipeline's counters
 // ==========================================================================
 template <int KIND, bool EVD>
-__global__ __launch_bounds__(256) void k_fg_count(MaskView m, int H, int W, int32_t *blkcnt, int nblk,
-                                                  int32_t *zero, int64_t zero_words) {
+__global__ __launch_bounds__(256) void k_fg_count(MaskView m, int H, int W, int32_t *blkcnt, uint64_t *fgbits,
+                                                  int nblk, int32_t *zero, int64_t zero_words) {
+    static_assert(kCompactChunk == 256, "one pixel per thread");
     const int b = blockIdx.y, blk = blockIdx.x;
     const int64_t P = (int64_t)H * W;
     {   // zero counts + tickets (read only by later kernels of this pipeline)
@@ -258,16 +255,11 @@ __global__ __launch_bounds__(256) void k_fg_count(MaskView m, int H, int W, int3
         for (int64_t i = g; i < zero_words; i += G) zero[i] = 0;
     }
     __shared__ int sh[8];
-    bool f[kCompactChunk / 256];
-#pragma unroll
-    for (int k = 0; k < kCompactChunk / 256; ++k) {
-        int64_t p = (int64_t)blk * kCompactChunk + k * 256 + threadIdx.x;
-        f[k] = p < P && is_fg<KIND, EVD>(m, b, (int)((uint32_t)p / (uint32_t)W), (int)((uint32_t)p % (uint32_t)W));
-    }
-    int c = 0;
-#pragma unroll
-    for (int k = 0; k < kCompactChunk / 256; ++k) c += f[k];
-    int2 t = block_sum2(c, 0, sh);
+    const int64_t p = (int64_t)blk * kCompactChunk + threadIdx.x;
+    const bool f = p < P && is_fg<KIND, EVD>(m, b, (int)((uint32_t)p / (uint32_t)W), (int)((uint32_t)p % (uint32_t)W));
+    const uint64_t bal = ballot(f);
+    if (lane_id() == 0) fgbits[((int64_t)b * nblk + blk) * 4 + threadIdx.x / 64] = bal;
+    int2 t = block_sum2(f ? 1 : 0, 0, sh);
     if (threadIdx.x == 0) blkcnt[b * nblk + blk] = t.x;
 }
 
@@ -300,20 +292,26 @@ struct VertexView {
     const void *p;
     int kind;
     int64_t s[5];
+    int32_t extent;     // bytes spanned by one image's [h,w,vn,2] view (< 2^31: buffer-load range)
 };
 
-template <int KIND, bool EVD>
+constexpr int kCompactKp = 12;   // keypoints whose vertex loads a compaction thread keeps in flight at once
+
+template <int KIND, bool EVD, int VK>
 __global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int H, int W, int vn,
-                                                 const int32_t *blkcnt, int32_t *dsagg, int nblk, int min_num,
-                                                 int max_num, uint64_t seed, const uint8_t *keep, int32_t *tn,
-                                                 int32_t *fgtot, float4 *pex, float4 *pix, uint32_t *exotic,
-                                                 int64_t nchv) {
-    constexpr int K = kCompactChunk / 256;
+                                                 const int32_t *blkcnt, const uint64_t *fgbits, int32_t *dsagg,
+                                                 int nblk, int min_num, int max_num, uint64_t seed,
+                                                 const uint8_t *keep, int32_t *tn, int32_t *fgtot, float4 *pex) {
+    static_assert(kCompactChunk == 256, "one pixel per thread");
     const int b = blockIdx.y, blk = blockIdx.x;
     const int64_t P = (int64_t)H * W;
+    const int wid = threadIdx.x / 64, lane = lane_id();
     __shared__ int sh[8];
-    __shared__ int wcnt[K][4];
+    __shared__ int wcnt[4];
     cstamp(blk, 0);
+    // one round trip: this wave's foreground ballot (k_fg_count) beside the
+    // image's per-block counts (the total and this block's row-major offset)
+    const uint64_t fw = fgbits[((int64_t)b * nblk + blk) * 4 + wid];
     int2 tot = image_totals(blkcnt + b * nblk, nblk, blk, sh);
     cstamp(blk, 1);
     const int fgb = tot.x;
@@ -327,33 +325,45 @@ __global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int 
         tn[b] = fgb;
         fgtot[b] = fgb;
     }
-    const float thr = ds ? (float)max_num / (float)fgb : 0.f;
-    const int wid = threadIdx.x / 64;
-    __shared__ int sel[kCompactChunk];   // block-local pixel index of the k-th selected pixel
-    bool f[K];
+    const uint32_t p = (uint32_t)blk * kCompactChunk + threadIdx.x;   // H, W <= 65535: fits
+    bool f = (fw >> lane) & 1;
+    if (ds && f) f = keep ? keep[b * P + p] != 0 : rand_unit(seed, (uint64_t)b * P + p) < (float)max_num / (float)fgb;
+    const uint64_t bal = ds ? ballot(f) : fw;
+    const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+    if (lane == 0) wcnt[wid] = __popcll(bal);
+    // this pixel's vertex loads (all keypoints of a group in flight together),
+    // issued before the block's offsets are known: buffer loads through a
+    // per-image descriptor, one VGPR offset for the pixel and the keypoint /
+    // component plane offsets in SGPRs (host check: the image's view spans
+    // < 2 GiB)
+    const int r = (int)(p / (uint32_t)W), c = (int)(p - (uint32_t)r * W);
+    constexpr int ES = VK == PV_VERTEX_F32 ? 4 : 2;
+    const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)((const char *)vx.p + (int64_t)b * vx.s[0] * ES), (short)0, vx.extent, 0x00020000);
+    const int voff = (int)((r * vx.s[1] + c * vx.s[2]) * ES);
+    float nx[kCompactKp], ny[kCompactKp];
+    auto load_group = [&](int v0) {
 #pragma unroll
-    for (int k = 0; k < K; ++k) {        // all mask reads in flight together
-        const int64_t p = (int64_t)blk * kCompactChunk + k * 256 + threadIdx.x;
-        f[k] = p < P && is_fg<KIND, EVD>(m, b, (int)((uint32_t)p / (uint32_t)W), (int)((uint32_t)p % (uint32_t)W));
-    }
-    int below[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const int64_t p = (int64_t)blk * kCompactChunk + k * 256 + threadIdx.x;
-        if (ds && f[k]) f[k] = keep ? keep[b * P + p] != 0 : rand_unit(seed, (uint64_t)b * P + p) < thr;
-        const uint64_t bal = ballot(f[k]);
-        below[k] = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-        if (lane_id() == 0) wcnt[k][wid] = __popcll(bal);
-    }
+        for (int u = 0; u < kCompactKp; ++u) {
+            nx[u] = ny[u] = 0.f;
+            if (f && v0 + u < vn) {
+                const int so = uniform((int)((v0 + u) * vx.s[3] * ES));
+                const int s4 = uniform((int)(vx.s[4] * ES));
+                if constexpr (VK == PV_VERTEX_F32) {
+                    nx[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vr, voff, so, 0));
+                    ny[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vr, voff, so + s4, 0));
+                } else {
+                    nx[u] = __half2float(__ushort_as_half(__builtin_amdgcn_raw_buffer_load_b16(vr, voff, so, 0)));
+                    ny[u] = __half2float(__ushort_as_half(__builtin_amdgcn_raw_buffer_load_b16(vr, voff, so + s4, 0)));
+                }
+            }
+        }
+    };
+    load_group(0);
     __syncthreads();
-    int nsel = 0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        int off = nsel;
-        for (int q = 0; q < wid; ++q) off += wcnt[k][q];
-        if (f[k]) sel[off + below[k]] = k * 256 + threadIdx.x;
-        nsel += wcnt[k][0] + wcnt[k][1] + wcnt[k][2] + wcnt[k][3];
-    }
+    const int nsel = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    int off = below;
+    for (int q = 0; q < wid; ++q) off += wcnt[q];
     if (ds) {
         // Downsampled offsets by look-back: publish this block's kept count
         // (+1, so 0 = not yet; k_fg_count zeroed the array), then add up the
@@ -373,53 +383,24 @@ __global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int 
         base = block_sum2(pre, 0, sh).x;
         if (blk == nblk - 1 && threadIdx.x == 0) { tn[b] = base + nsel; fgtot[b] = fgb; }
     }
-    __syncthreads();
     cstamp(blk, 2);
-    // (selected pixel, keypoint) items: consecutive threads take consecutive
-    // pixels of one keypoint, so vertex reads and pex/pix writes coalesce
+    // the selected pixel's records at t = base + its rank: consecutive
+    // selected pixels write consecutive records of each keypoint
     float4 *eb = pex + (int64_t)b * vn * P;
-    float4 *pb = pix + (int64_t)b * vn * P;
-    const int nitem = nsel * vn;
-    constexpr int U = 4;                 // items per thread in flight
-    for (int it0 = threadIdx.x; it0 < nitem; it0 += 256 * U) {
-        float nx[U], ny[U];
-        int vv[U], kk[U], rr[U], cc[U];
+    const int64_t t = base + off;
+    for (int v0 = 0; v0 < vn; v0 += kCompactKp) {
+        if (v0 > 0) load_group(v0);
+        if (f) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int it = it0 + 256 * u;
-            nx[u] = ny[u] = 0.f;
-            vv[u] = -1;
-            if (it < nitem) {
-                const int v = it / nsel, k = it - v * nsel;
-                const uint32_t p = (uint32_t)blk * kCompactChunk + sel[k];   // H, W <= 65535: fits
-                const int r = (int)(p / (uint32_t)W), c = (int)(p - (uint32_t)r * W);
-                const int64_t vo = b * vx.s[0] + r * vx.s[1] + c * vx.s[2] + v * vx.s[3];
-                if (vx.kind == PV_VERTEX_F32) {
-                    nx[u] = ((const float *)vx.p)[vo];
-                    ny[u] = ((const float *)vx.p)[vo + vx.s[4]];
-                } else {
-                    nx[u] = __half2float(((const __half *)vx.p)[vo]);
-                    ny[u] = __half2float(((const __half *)vx.p)[vo + vx.s[4]]);
-                }
-                vv[u] = v; kk[u] = k; rr[u] = r; cc[u] = c;
+            for (int u = 0; u < kCompactKp; ++u) {
+                if (v0 + u >= vn) break;
+                const int64_t o = (int64_t)(v0 + u) * P + t;
+                // the reference's operands only: the vote kernel makes the fast
+                // test's (prep_compacted) while it stages them
+                eb[o] = make_float4((float)c, (float)r, nx[u], ny[u]);
             }
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (vv[u] < 0) continue;
-            const int64_t t = base + kk[u];
-            const int64_t o = (int64_t)vv[u] * P + t;
-            eb[o] = make_float4((float)cc[u], (float)rr[u], nx[u], ny[u]);
-            // fast-test data: exact norm1 validity (KU:119-121); the direction
-            // rounded per component (any positive scale: rsq)
-            const float n1 = sqrtf(nx[u] * nx[u] + ny[u] * ny[u]);
-            const bool valid = !((double)n1 < 1e-6);
-            const float rs = __builtin_amdgcn_rsqf(fmaf(nx[u], nx[u], ny[u] * ny[u]));
-            pb[o] = make_float4(valid ? (float)cc[u] : __builtin_nanf(""), (float)rr[u], nx[u] * rs, ny[u] * rs);
-            if (valid && !(n1 <= kN1Max)) atomicOr(&exotic[b * nchv + t / kVoteChunk], 1u);
-        }
     }
-    __syncthreads();
     cstamp(blk, 3);
 }
 
@@ -427,9 +408,10 @@ __global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int 
 // K4: hypotheses (KU:11-49) + fused vote/count.
 // counts[b][v][h] += #{t : inlier(h, v, t)}.
 //
-// k_hyp_gen makes every hypothesis once (pixel pairs from the caller or the
-// counter RNG, RV:553) and stores it in the reference layout (refine stage,
-// diagnostics) and keypoint-major (the vote's coalesced reads).
+// In the pipeline the vote kernel makes its own hypotheses (pixel pairs from
+// the caller or the counter RNG, RV:553; item_hyp) in its prologue, beside
+// its first pixel loads; the unit whose range starts at pixel 0 of a (b, v,
+// group) stores them in the reference layout (refine stage, diagnostics).
 //
 // k_vote_count: lane = hypothesis (kHypLane = 2 per lane, groups of 128 per
 // wave); the (image, keypoint, group, pixel) space is cut into equal
@@ -464,21 +446,18 @@ __device__ __forceinline__ T *uptr(T *p) {
 }
 
 struct VoteArgs {
-    const float4 *pix;          // PREPPED: fast data (fx, cy, ux, uy): pix[(b*vn + v)*P + t]
     const float4 *pex;          // PREPPED: exact data (cx, cy, nx, ny), same layout
-    const uint32_t *exotic;     // PREPPED: 256-pixel chunk holds a pixel outside the fast domain
     const float2 *coords;       // !PREPPED: coords[b*P + t]
     const float2 *raw;          // !PREPPED: raw[b*vn*P + v*raw_v + t*raw_t]
     const float2 *hyp;          // !GEN: hyp[b*hyp_sb + v*hyp_sv + h*hyp_sh]
     float2 *hyp_out;            // GEN: generated hypotheses [b][nh][vn]
-    float2 *hypv_out;           // GEN: optional keypoint-major copy [b][vn][nh]
     int64_t hyp_sb, hyp_sv, hyp_sh;
     float *diag_hyp;            // GEN: optional copy [b][nh][vn][2]
     const int32_t *idxs;        // GEN: pixel pairs [b][nh][vn][2], or nullptr (counter RNG)
     int32_t *counts;            // counts[b*cnt_bs + v*cnt_v + h*cnt_h]
     const int32_t *tn_dev;      // [b] pixels per image, or nullptr (tn_host)
     uint64_t seed;
-    int32_t P, raw_v, raw_t, exotic_b, cnt_v, cnt_h, cnt_bs;
+    int32_t P, raw_v, raw_t, cnt_v, cnt_h, cnt_bs;
     int32_t tn_host, b, vn, nh, hgn, fast;
     float thr, tau, gzf, gzr;
     uint64_t *trace;            // debug: per-wave (start, end) s_memrealtime stamps, or nullptr
@@ -537,7 +516,6 @@ __device__ __forceinline__ float2 item_hyp(const VoteArgs &a, int b, int v, int 
             if (exact_intersect(e0.z, e0.w, e0.x, e0.y, e1.z, e1.w, e1.x, e1.y, &ox, &oy)) { x = ox; y = oy; }
             if (store) {
                 a.hyp_out[gid] = make_float2(x, y);
-                if (a.hypv_out) a.hypv_out[((int64_t)b * a.vn + v) * a.nh + h] = make_float2(x, y);
                 if (a.diag_hyp) { a.diag_hyp[gid * 2] = x; a.diag_hyp[gid * 2 + 1] = y; }
             }
         }
@@ -546,21 +524,6 @@ __device__ __forceinline__ float2 item_hyp(const VoteArgs &a, int b, int v, int 
         x = q.x; y = q.y;
     }
     return make_float2(x, y);
-}
-
-// Hypotheses once per launch, one thread per (image, hypothesis, keypoint):
-// the pixel pair (the caller's idxs or the counter RNG, RV:553) and its
-// intersection (KU:11-49), stored in both layouts; images without a vote
-// (tn 0) are left alone.
-__global__ __launch_bounds__(256) void k_hyp_gen(VoteArgs a) {
-    const int64_t per = (int64_t)a.nh * a.vn;
-    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (gid >= per * a.b) return;
-    const int b = (int)(gid / per);
-    const int r = (int)(gid - b * per);
-    const int h = r / a.vn, v = r - h * a.vn;
-    const int n = a.tn_dev ? a.tn_dev[b] : a.tn_host;
-    if (n > 0) item_hyp<true, true>(a, b, v, h, true, n, true);
 }
 
 // wave w's share [lo, hi) of `total` items cut evenly over `nwaves` (32-bit: the callers keep total < 2^31)
@@ -603,6 +566,18 @@ __device__ __forceinline__ float4 prep_pixel(float cx, float cy, float nx, float
     bool ok = !((double)n1 < 1e-6);
     double N = sqrt((double)nx * nx + (double)ny * ny);
     return make_float4(ok ? cx : __builtin_nanf(""), cy, (float)(nx / N), (float)(ny / N));
+}
+
+// fast data of a compacted pipeline pixel (cx, cy, nx, ny), made while the
+// vote kernel stages it: validity by the reference's own norm1 (KU:119-121),
+// the direction rounded per component after scaling by rsq (the fast test
+// needs only its direction); *exo: votes, but outside the fast domain
+__device__ __forceinline__ float4 prep_compacted(const F4 &e, bool *exo) {
+    const float n1 = sqrtf(e.z * e.z + e.w * e.w);
+    const bool valid = !((double)n1 < 1e-6);
+    const float rs = __builtin_amdgcn_rsqf(fmaf(e.z, e.z, e.w * e.w));
+    *exo = valid && !(n1 <= kN1Max);
+    return make_float4(valid ? e.x : __builtin_nanf(""), e.y, e.z * rs, e.w * rs);
 }
 
 __device__ __forceinline__ bool pixel_exotic(float nx, float ny) {
@@ -670,7 +645,7 @@ struct QuarterBoxes {
 // sub-chunk's first pixel (known to every wave without a reduction); the
 // quarter boxes come through LDS.
 template <bool PREPPED, bool SH>
-__device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED> *slabs, QuarterBoxes *qbs, int &buf, int b, int v, int hg,
+__device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED> *slabs, QuarterBoxes *qbs, float2 *hlds, int &buf, int b, int v, int hg,
                                              int ts, int te, int n, uint32_t rem_after, uint32_t prio_hi, uint32_t prio_mid, int &nfix,
                                              uint64_t &tloop) {
     const int lane = lane_id();
@@ -690,36 +665,31 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
     constexpr float kBig = 3.0e38f;
 
     // SH: the loads of a sub-chunk (this thread's pixel, the first pixel for
-    // the origin, the exotic flags); the first sub-chunk's are issued before
-    // the hypothesis generation so that the two memory round trips overlap
+    // the origin); the first sub-chunk's are issued before the hypothesis
+    // generation so that the two memory round trips overlap
     struct SubLoad {
-        F4 f0, e, q;
-        uint32_t exf;
+        F4 f0, e;
     };
     auto load_sub = [&](int s0, int np) {
         SubLoad L;
         const int t = wid * kWave + lane;
         L.f0 = pixel_exact<PREPPED>(a, b, v, s0);
         L.e = F4{0.f, 0.f, 0.f, 0.f};
-        L.q = F4{__builtin_nanf(""), 0.f, 0.f, 0.f};
-        if (t < np) {
-            L.e = pixel_exact<PREPPED>(a, b, v, s0 + t);
-            if (PREPPED) {
-                const float4 f = a.pix[((int64_t)b * a.vn + v) * a.P + s0 + t];
-                L.q = F4{f.x, f.y, f.z, f.w};
-            }
-        }
-        L.exf = 0;
-        if (PREPPED) {
-            const uint32_t *exb = a.exotic + (int64_t)b * a.exotic_b;
-            L.exf = exb[s0 / kVoteChunk] | exb[(s0 + np - 1) / kVoteChunk];
-        }
+        if (t < np) L.e = pixel_exact<PREPPED>(a, b, v, s0 + t);
         return L;
     };
     SubLoad L;               // (loaded at the end of the previous sub-chunk: not live across its hot loop)
     if (SH) L = load_sub(ts, min(kVoteChunk, te - ts));
 
-    float2 he[kHypLane];     // exact hypotheses (the reference's operands)
+    // exact hypotheses (the reference's operands): SH keeps them in the wave's
+    // LDS row (read per sub-chunk and by the rare exact decisions), which
+    // frees their registers for the hot loop
+    float2 he_r[kHypLane];
+    auto he_set = [&](int i, float2 x) {
+        if (SH) hlds[i * kWave + lane] = x;
+        else he_r[i] = x;
+    };
+    auto he = [&](int i) -> float2 { return SH ? hlds[i * kWave + lane] : he_r[i]; };
     bool hf[kHypLane];       // decided by the fast test
     bool hxo[kHypLane];      // outside the fast test's domain: exact only
     int cnt[kHypLane];
@@ -728,12 +698,17 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
         const int h = hg * kGroup + i * kWave + lane;
         const bool hl = h < a.nh;
 #ifndef PVVOTE_ABLATE_HYP
-        he[i] = item_hyp<false, PREPPED>(a, b, v, h, hl, n, false);
+        // the pipeline (PREPPED) makes its hypotheses here: every block of
+        // (b, v, group) intersects the same pixel pairs, the one whose range
+        // starts at pixel 0 stores them (reference layout, for the refine /
+        // EVD stages and the diagnostics); the API path reads the caller's
+        const float2 hv = item_hyp<PREPPED, PREPPED>(a, b, v, h, hl, n, PREPPED && ts == 0);
 #else
-        he[i] = make_float2(300.f + 0.37f * lane + 0.11f * v, 200.f + 0.23f * i + 0.5f * hg);
+        const float2 hv = make_float2(300.f + 0.37f * lane + 0.11f * v, 200.f + 0.23f * i + 0.5f * hg);
 #endif
-        const bool fin = isfinite(he[i].x) && isfinite(he[i].y);    // non-finite: never an inlier
-        hxo[i] = hl && fin && hyp_exact_only(he[i].x, he[i].y);
+        he_set(i, hv);
+        const bool fin = isfinite(hv.x) && isfinite(hv.y);    // non-finite: never an inlier
+        hxo[i] = hl && fin && hyp_exact_only(hv.x, hv.y);
         hf[i] = hl && fin && !hxo[i];
         cnt[i] = 0;
     }
@@ -754,12 +729,15 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
             ox = floorf(L.f0.x);
             oy = floorf(L.f0.y);
             if (!(fabsf(ox) <= 1.6e7f && fabsf(oy) <= 1.6e7f)) { ox = 0.f; oy = 0.f; }
-            F4 q = L.q;
+            F4 q{__builtin_nanf(""), 0.f, 0.f, 0.f};
             float xl = kBig, xh = -kBig;
             bool exo_p = false;
             if (t < np) {
                 const F4 e = L.e;
-                if (!PREPPED) {
+                if (PREPPED) {
+                    const float4 f = prep_compacted(e, &exo_p);
+                    q = F4{f.x, f.y, f.z, f.w};
+                } else {
                     const float4 f = prep_pixel(e.x, e.y, e.z, e.w);
                     q = F4{f.x, f.y, f.z, f.w};
                     exo_p = pixel_exotic(e.z, e.w);
@@ -805,7 +783,7 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
                 cyl = fminf(cyl, Q.z); cyh = fmaxf(cyh, Q.w);
                 ex |= QB.exo[k];
             }
-            slow |= (PREPPED ? L.exf : ex) != 0;
+            slow |= ex != 0;
             slow = __builtin_amdgcn_readfirstlane(slow);
             const float ax = fmaxf(cxh - ox, ox - cxl), ay = fmaxf(cyh - oy, oy - cyl);
             R = __builtin_amdgcn_sqrtf(fmaf(ax, ax, ay * ay)) * 1.00001f;
@@ -822,8 +800,10 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
             if (j < np) {
                 const F4 e = pixel_exact<PREPPED>(a, b, v, s0 + j);
                 if (PREPPED) {
-                    const float4 f = a.pix[((int64_t)b * a.vn + v) * a.P + s0 + j];
+                    bool xo;
+                    const float4 f = prep_compacted(e, &xo);
                     q = F4{f.x, f.y, f.z, f.w};
+                    exo_p |= xo;
                 } else {
                     const float4 f = prep_pixel(e.x, e.y, e.z, e.w);
                     q = F4{f.x, f.y, f.z, f.w};
@@ -835,12 +815,7 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
             }
             q4[k] = q;
         }
-        if (PREPPED) {
-            const uint32_t *ex = a.exotic + (int64_t)b * a.exotic_b;
-            slow |= (ex[s0 / kVoteChunk] | ex[(s0 + np - 1) / kVoteChunk]) != 0;
-        } else {
-            slow |= __builtin_amdgcn_ballot_w64(exo_p) != 0;
-        }
+        slow |= __builtin_amdgcn_ballot_w64(exo_p) != 0;
         slow = __builtin_amdgcn_readfirstlane(slow);
         // per-quarter bounding boxes (lane k of qxl..qyh holds quarter k); the
         // compacted pixels are row-major, so a quarter's rows run from its
@@ -882,8 +857,9 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
         float hx[kHypLane], hy[kHypLane], Bv[kHypLane], gd[kHypLane];
 #pragma unroll
         for (int i = 0; i < kHypLane; ++i) {
-            hx[i] = hf[i] ? he[i].x - ox : __builtin_nanf("");
-            hy[i] = hf[i] ? he[i].y - oy : __builtin_nanf("");
+            const float2 hv = he(i);
+            hx[i] = hf[i] ? hv.x - ox : __builtin_nanf("");
+            hy[i] = hf[i] ? hv.y - oy : __builtin_nanf("");
             Bv[i] = (__builtin_amdgcn_sqrtf(fmaf(hx[i], hx[i], hy[i] * hy[i])) + R) * 1.00001f + 1e-30f;
             gd[i] = 0.f;
         }
@@ -922,10 +898,11 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
 #pragma unroll 1
                 for (int pi = 0; pi < 4 * kHypLane; ++pi) {
                     const int p = pi / kHypLane, i = pi % kHypLane;
-                    float hxi = hx[0], hyi = hy[0], gdi = gd[0], ex = he[0].x, ey = he[0].y;
+                    const float2 h0 = he(0);
+                    float hxi = hx[0], hyi = hy[0], gdi = gd[0], ex = h0.x, ey = h0.y;
 #pragma unroll
                     for (int k = 1; k < kHypLane; ++k) {
-                        if (i == k) { hxi = hx[k]; hyi = hy[k]; gdi = gd[k]; ex = he[k].x; ey = he[k].y; }
+                        if (i == k) { const float2 hk = he(k); hxi = hx[k]; hyi = hy[k]; gdi = gd[k]; ex = hk.x; ey = hk.y; }
                     }
                     const float zz = zval(stage[j + p], hxi, hyi);
                     const bool u = fabsf(zz) <= gdi;
@@ -1028,7 +1005,9 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
                 while (m) {
                     const int l = __builtin_ctzll(m);
                     m &= m - 1;
-                    const float ex = bcast(he[i].x, l), ey = bcast(he[i].y, l);
+                    float ex, ey;
+                    if (SH) { const float2 hl2 = hlds[i * kWave + l]; ex = hl2.x; ey = hl2.y; }
+                    else { ex = bcast(he_r[i].x, l); ey = bcast(he_r[i].y, l); }
                     int c = 0;
 #pragma unroll
                     for (int k = 0; k < kVoteChunk / kWave; ++k) {
@@ -1049,7 +1028,10 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
             for (int j = 0; j < np; ++j) {
                 const F4 e = stagex.get(j);
 #pragma unroll
-                for (int i = 0; i < kHypLane; ++i) cnt[i] += exact_vote(e.z, e.w, e.x, e.y, he[i].x, he[i].y, a.thr);
+                for (int i = 0; i < kHypLane; ++i) {
+                    const float2 hv = he(i);
+                    cnt[i] += exact_vote(e.z, e.w, e.x, e.y, hv.x, hv.y, a.thr);
+                }
             }
         }
         if (!SH) __builtin_amdgcn_wave_barrier();
@@ -1087,6 +1069,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     __builtin_amdgcn_s_setprio(3);
     __shared__ VoteSlab<PREPPED> slab_all[SH ? 2 : 4];
     __shared__ QuarterBoxes qb_all[SH ? 2 : 1];
+    __shared__ float2 hyp_all[SH ? 4 * kGroup : 1];   // SH: each wave's exact hypotheses
     VoteSlab<PREPPED> *slabs = SH ? slab_all : slab_all + threadIdx.x / 64;
     int buf = 0;
     const int ggn = a.hgn / gpu;          // unit groups per keypoint
@@ -1116,7 +1099,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         const int te = (int)min((uint32_t)n, ts + (hi - lo));
         const int v = g / ggn, gg = g - v * ggn;
         const int hg = SH ? gg * 4 + (int)__builtin_amdgcn_readfirstlane(threadIdx.x / 64) : gg;
-        vote_segment<PREPPED, SH>(a, slabs, qb_all, buf, uniform(b), uniform(v), uniform(hg), uniform(ts), uniform(te), n,
+        vote_segment<PREPPED, SH>(a, slabs, qb_all, SH ? hyp_all + (threadIdx.x / 64) * kGroup : hyp_all, buf, uniform(b), uniform(v), uniform(hg), uniform(ts), uniform(te), n,
                                        uniform((int)((hi - lo) - (uint32_t)(te - ts))), prio_hi, prio_mid, nfix, tloop);
         lo += te - ts;
         ++nseg;
@@ -1185,6 +1168,12 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
         const int t = t0 + u * tstep;
         e[u] = t < n ? eb[t] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    // the keypoint's hypotheses too (the winner's is then read from LDS, not
+    // fetched after the argmax: one memory round trip fewer)
+    constexpr int kRefineLdsHyp = 1024;
+    __shared__ float2 shyp[kRefineLdsHyp];
+    if (nh <= kRefineLdsHyp && n > 0)
+        for (int h = threadIdx.x; h < nh; h += 256) shyp[h] = hyp[((int64_t)b * nh + h) * vn + v];
     // argmax over h, first index on ties: key = count << 32 | ~h
     uint64_t key = 0;
     const int32_t *cnt = counts + ((int64_t)b * vn + v) * nh;
@@ -1205,7 +1194,7 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
     // RV:570-575: ratio = count / tn; best starts at 0 and is replaced only on a strict increase
     const float ratio = n > 0 ? (float)wcnt / (float)n : 0.f;
     float2 best = make_float2(0.f, 0.f);
-    if (n > 0 && 0.f < ratio) best = hyp[((int64_t)b * nh + win) * vn + v];
+    if (n > 0 && 0.f < ratio) best = nh <= kRefineLdsHyp ? shyp[win] : hyp[((int64_t)b * nh + win) * vn + v];
     double acc[5] = {0, 0, 0, 0, 0};
     auto accum = [&](const float4 &q) {   // (cx, cy, nx, ny)
         if (exact_vote(q.z, q.w, q.x, q.y, best.x, best.y, thr)) {
@@ -2470,11 +2459,16 @@ template <int KIND, bool EVD>
 struct CompactStage {
     static int run(const CompactArgs *a) {
         dim3 grid(a->nblk, a->b);
-        k_fg_count<KIND, EVD><<<grid, 256, 0, a->s>>>(a->m, a->H, a->W, a->ws.blkcnt, a->nblk, a->ws.counts,
+        k_fg_count<KIND, EVD><<<grid, 256, 0, a->s>>>(a->m, a->H, a->W, a->ws.blkcnt, a->ws.fgbits, a->nblk, a->ws.counts,
                                                       a->ws.zero_words);
-        k_compact<KIND, EVD><<<grid, 256, 0, a->s>>>(a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.dsagg,
+        if (a->vx.kind == PV_VERTEX_F32)
+            k_compact<KIND, EVD, PV_VERTEX_F32><<<grid, 256, 0, a->s>>>(a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.fgbits, a->ws.dsagg,
                                                      a->nblk, a->min_num, a->max_num, a->seed, a->keep, a->ws.tn,
-                                                     a->ws.fgtot, a->ws.pex, a->ws.pix, a->ws.exotic, a->ws.nchv);
+                                                     a->ws.fgtot, a->ws.pex);
+        else
+            k_compact<KIND, EVD, PV_VERTEX_F16><<<grid, 256, 0, a->s>>>(a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.fgbits, a->ws.dsagg,
+                                                     a->nblk, a->min_num, a->max_num, a->seed, a->keep, a->ws.tn,
+                                                     a->ws.fgtot, a->ws.pex);
         return last();
     }
 };
@@ -2500,6 +2494,17 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
     ca.vx.p = img->vertex;
     ca.vx.kind = img->vertex_kind;
     for (int i = 0; i < 5; ++i) ca.vx.s[i] = img->vertex_strides[i];
+    {   // bytes one image's view spans (the compaction's buffer-load range)
+        const int64_t es = img->vertex_kind == PV_VERTEX_F32 ? 4 : 2;
+        int64_t hi = 0;
+        const int64_t dims[5] = {1, H, W, vn, 2};
+        for (int i = 1; i < 5; ++i) {
+            if (ca.vx.s[i] < 0) return PV_EINVAL;
+            hi += (dims[i] - 1) * ca.vx.s[i];
+        }
+        if ((hi + 1) * es > INT32_MAX) return PV_EINVAL;
+        ca.vx.extent = (int32_t)((hi + 1) * es);
+    }
     ca.b = b; ca.H = H; ca.W = W; ca.vn = vn; ca.nblk = nblk;
     ca.min_num = prm->min_num; ca.max_num = prm->max_num;
     ca.seed = mix64(prm->seed ^ 0xd1b54a32d192ed03ull);
@@ -2509,8 +2514,7 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
     int r = dispatch_mask<CompactStage>(img->mask_kind, evd, (const CompactArgs *)&ca);
     if (r) return r;
     VoteArgs va{};
-    va.pix = w.pix; va.pex = w.pex; va.P = (int32_t)P;
-    va.exotic = w.exotic; va.exotic_b = (int32_t)w.nchv;
+    va.pex = w.pex; va.P = (int32_t)P;
     va.hyp = nullptr;
     va.hyp_out = w.hyp; va.diag_hyp = dg.hyp;
     va.idxs = prm->idxs; va.seed = mix64(prm->seed);
@@ -2519,15 +2523,9 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
     va.b = b; va.vn = vn; va.nh = nh; va.hgn = (nh + kGroup - 1) / kGroup;
     fast_constants(prm->inlier_thresh, &va);
     va.trace = g_vote_trace;
-    // hypotheses first, once each (one kernel for the batch); the vote
-    // kernel reads them keypoint-major
-    va.hypv_out = w.hypv;
-    {
-        const int64_t nt = (int64_t)b * nh * vn;
-        k_hyp_gen<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(va);
-        if ((r = last())) return r;
-    }
-    va.hyp = w.hypv; va.hyp_sb = (int64_t)vn * nh; va.hyp_sv = nh; va.hyp_sh = 1;
+    // the vote kernel generates the hypotheses itself (item_hyp in its
+    // prologue, overlapped with its first pixel loads) and stores them in
+    // the reference layout; no separate hypothesis launch
     if (dg.ev_vote_begin) {
         hipError_t e = hipEventRecord((hipEvent_t)dg.ev_vote_begin, s);
         if (e != hipSuccess) return rc(e);
@@ -2541,10 +2539,10 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
         VoteArgs vc = va;
         const int nb = std::min(chunk, b - b0);
         vc.b = nb;
-        vc.pix += (int64_t)b0 * vn * P;
         vc.pex += (int64_t)b0 * vn * P;
-        vc.exotic += (int64_t)b0 * va.exotic_b;
-        vc.hyp += b0 * vc.hyp_sb;
+        vc.hyp_out += (int64_t)b0 * nh * vn;
+        if (vc.diag_hyp) vc.diag_hyp += (int64_t)b0 * nh * vn * 2;
+        if (vc.idxs) vc.idxs += (int64_t)b0 * nh * vn * 2;
         vc.counts += (int64_t)b0 * va.cnt_bs;
         vc.tn_dev += b0;
         launch_vote<true>(vc, nb * per_img, s);
