@@ -501,5 +501,101 @@ def main_motion():
     motion_cases(RV)
 
 
+# YCB-Video intrinsics (lib/data_utils_xin.py:1723) and 21 keypoints per object
+# (lib/datasets/YCB_dataset.py:185): BASELINE configs[4].
+K_YCB = np.array([[1066.8, 0.0, 320.0], [0.0, 1066.8, 240.0], [0.0, 0.0, 1.0]])
+
+
+def ycb_object():
+    """21 model keypoints (a 0.12 m object) and a pose 1 m in front of the YCB
+    camera; the projected keypoints fall inside the 480x640 frame."""
+    rng = np.random.default_rng(2100)
+    pts3d = rng.uniform(-0.06, 0.06, (21, 3))
+    rv = np.array([0.4, -0.3, 0.25])
+    th = np.linalg.norm(rv)
+    k = rv / th
+    Kx = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    R = np.eye(3) + np.sin(th) * Kx + (1 - np.cos(th)) * Kx @ Kx
+    pose = np.concatenate([R, np.array([[0.01], [-0.02], [1.0]])], 1)
+    return pts3d, pose, synth.project(pts3d, pose, K_YCB)
+
+
+def _u16(a):
+    a = np.asarray(a)
+    assert a.min() >= 0 and a.max() < 65536
+    return a.astype(np.uint16)
+
+
+def ycb_cases(RV, stub):
+    """configs[4] shapes: vn = 21 through v3 (hn 512) and EVD with mean (16 x
+    256 hypotheses) on a 480x640 frame whose keypoints are the projection of
+    a known pose; and the EVD branches on small frames (vn 21): a normal image,
+    one with foreground < min_num (RV:343-348: zero hypotheses, ratio 1) and
+    one with foreground > max_num (RV:351-355: downsampled, foreground
+    re-counted), with mean and topk variants."""
+    out = {}
+    pts3d, pose, p2d = ycb_object()
+    f = synth.synthetic_field(2101, vn=21, keypoints=p2d, center=(float(p2d[:, 0].mean()), float(p2d[:, 1].mean())))
+    m = torch.argmax(torch.from_numpy(f["seg"]), 1)
+    vv = torch.from_numpy(f["vertex"]).permute(0, 2, 3, 1).reshape(1, 480, 640, 21, 2)
+    out.update(seed=2101, points_3d=pts3d, pose=pose, camera=K_YCB, points_2d=p2d, tn=f["tn"],
+               seg_sha=sha(f["seg"]), vertex_sha=sha(f["vertex"]))
+    torch.manual_seed(61)
+    stub.calls.clear()
+    kp = RV.ransac_voting_layer_v3(m, vv, 512, inlier_thresh=0.99).numpy()
+    idxs, hyps, counts, refc, coords = per_image_records(stub)
+    out.update(v3_keypoints=kp, v3_idxs=_u16(np.stack(idxs)), v3_hyp=np.stack(hyps),
+               v3_counts=_u16(np.stack(counts)), v3_refine_counts=np.stack(refc),
+               v3_iters=len(vote_calls(stub, "gen")))
+    print("ycb v3 max err vs projection", np.abs(kp[0] - p2d).max())
+    torch.manual_seed(62)
+    stub.calls.clear()
+    _, cov = RV.estimate_voting_distribution_with_mean(m, vv, torch.from_numpy(kp))
+    gens = vote_calls(stub, "gen")
+    out.update(evdm_cov=cov.numpy(), evdm_idxs=_u16(np.stack([g["idxs"] for g in gens]))[None])
+
+    # EVD branches on 40x48 frames, vn 21
+    H, W, vn = 40, 48, 21
+    kin = np.random.default_rng(70).uniform([4.0, 4.0], [44.0, 36.0], (3, vn, 2))   # keypoints in the frame
+    fa, va = small_field(71, vn=vn, radius=8.5, keypoints=kin[0])    # 225 px: voted as is
+    fb, vb = small_field(72, vn=vn, radius=1.5, keypoints=kin[1])    # 9 px < min_num = 20 -> skipped
+    fc, vc = small_field(73, vn=vn, radius=14.5, keypoints=kin[2])   # 665 px > max_num = 300 -> downsampled
+    masks = np.stack([fa["mask"], fb["mask"], fc["mask"]]).astype(np.int64)
+    verts = np.stack([va, vb, vc])
+    means = np.stack([fa["keypoints"], fb["keypoints"], fc["keypoints"]]).astype(np.float32)
+    out.update(br_mask=masks, br_vertex=verts, br_mean=means)
+    for name, seed in (("mean", 63), ("topk", 64)):
+        torch.manual_seed(seed)
+        stub.calls.clear()
+        if name == "mean":
+            _, cov = RV.estimate_voting_distribution_with_mean(torch.from_numpy(masks), torch.from_numpy(verts),
+                                                               torch.from_numpy(means), round_hyp_num=32,
+                                                               min_hyp_num=128, max_num=300)
+            out.update(br_mean_cov=cov.numpy())
+        else:
+            # the skipped image contributes round_hyp_num rows (RV:274), the
+            # others ceil(min/round) * round_hyp_num: one round keeps the cat legal;
+            # topk = all rows (ties at the k-th ratio are unspecified in torch.topk)
+            mu, cov = RV.estimate_voting_distribution(torch.from_numpy(masks), torch.from_numpy(verts),
+                                                      round_hyp_num=64, min_hyp_num=64, topk=64, min_num=20,
+                                                      max_num=300)
+            out.update(br_topk_mean=mu.numpy(), br_topk_cov=cov.numpy())
+        gens = vote_calls(stub, "gen")
+        per = len(gens) // 2                             # images 0 and 2 voted
+        keep = np.zeros((3, H, W), bool)
+        c = gens[per]["coords"]
+        keep[2, c[:, 1].astype(int), c[:, 0].astype(int)] = True
+        out.update({f"br_{name}_idxs": np.stack([np.stack([g["idxs"] for g in gens[:per]]),
+                                                  np.stack([g["idxs"] for g in gens[per:]])]),
+                    f"br_{name}_keep2": keep[2], f"br_{name}_tn": np.array([gens[0]["tn"], gens[per]["tn"]])})
+    save("ycb21_cases", **out)
+
+
+def main_ycb():
+    install_shims()
+    stub = TorchKernels()
+    ycb_cases(load_reference(stub), stub)
+
+
 if __name__ == "__main__":
-    {"v5": main_v5, "motion": main_motion}.get(sys.argv[1] if sys.argv[1:] else "", main)()
+    {"v5": main_v5, "motion": main_motion, "ycb": main_ycb}.get(sys.argv[1] if sys.argv[1:] else "", main)()

@@ -36,3 +36,15 @@ def synth_inputs(g):
     mask = np.argmax(f["seg"], 1).astype(np.int64)
     vertex = np.ascontiguousarray(f["vertex"].transpose(0, 2, 3, 1).reshape(1, 480, 640, 9, 2))
     return mask, vertex, f
+
+
+def ycb_inputs(g):
+    """configs[4] frame of ycb21_cases: 21 keypoints projected from a known
+    pose (YCB camera), int64 mask [1,h,w], vertex view [1,h,w,21,2], field."""
+    p2d = g["points_2d"]
+    f = synth.synthetic_field(int(g["seed"]), vn=21, keypoints=p2d,
+                              center=(float(p2d[:, 0].mean()), float(p2d[:, 1].mean())))
+    assert sha(f["seg"]) == str(g["seg_sha"]) and sha(f["vertex"]) == str(g["vertex_sha"]), "S(seed) drifted"
+    mask = np.argmax(f["seg"], 1).astype(np.int64)
+    vertex = np.ascontiguousarray(f["vertex"].transpose(0, 2, 3, 1).reshape(1, 480, 640, 21, 2))
+    return mask, vertex, f

@@ -533,3 +533,44 @@ def test_workspace_growth_inside_capture_raises(device, rvg):
     with pytest.raises(RuntimeError, match="graph capture"):
         with torch.cuda.graph(g):
             rvg.ransac_voting_layer_v3_from_network(seg, ver, 64, _workspace=rvg.VotingWorkspace(), _seed=1)
+
+
+# ---------------------------------------------------------------- configs[4]: 21 keypoints
+def test_ycb21_v3_and_evd_with_mean(device, rvg):
+    """vn = 21 (YCB, configs[4]) through v3 (hn 512, bit-exact counts and
+    hypotheses vs the reference's) and EVD with mean (16 x 256 hypotheses)."""
+    g = G.load("ycb21_cases")
+    mask, vertex, _ = G.ycb_inputs(g)
+    gg = {k[3:]: (g[k].astype(np.int32) if k in ("v3_idxs", "v3_counts") else g[k])
+          for k in g if k.startswith("v3_")}
+    kp, diag = run_v3(rvg, mask, vertex, gg, "", device)
+    assert int(diag["iters"][0]) == int(g["v3_iters"])
+    idxs = g["evdm_idxs"][0].astype(np.int32).reshape(1, -1, 21, 2)
+    _, cov = rvg.estimate_voting_distribution_with_mean(cu(mask, device), cu(vertex, device),
+                                                        cu(g["v3_keypoints"], device), _idxs=idxs)
+    np.testing.assert_allclose(cov.cpu().numpy(), g["evdm_cov"], rtol=COV_RTOL,
+                               atol=1e-4 * np.abs(g["evdm_cov"]).max())
+
+
+def test_ycb21_evd_branches(device, rvg):
+    """One batch with a normal image, one below min_num (RV:343-348) and one
+    above max_num (RV:351-355, the reference's keep-mask injected), both EVD
+    variants, against the reference's covariances."""
+    g = G.load("ycb21_cases")
+    m, v = cu(g["br_mask"], device), cu(g["br_vertex"], device)
+    for name in ("mean", "topk"):
+        ix = g[f"br_{name}_idxs"]
+        idxs = np.zeros((3, ix.shape[1] * ix.shape[2], 21, 2), np.int32)
+        idxs[0] = ix[0].reshape(-1, 21, 2)
+        idxs[2] = ix[1].reshape(-1, 21, 2)
+        keep = np.ones((3, 40, 48), np.uint8)
+        keep[2] = g[f"br_{name}_keep2"]
+        if name == "mean":
+            _, cov = rvg.estimate_voting_distribution_with_mean(m, v, cu(g["br_mean"], device), round_hyp_num=32,
+                                                                min_hyp_num=128, max_num=300, _idxs=idxs, _keep=keep)
+        else:
+            mu, cov = rvg.estimate_voting_distribution(m, v, round_hyp_num=64, min_hyp_num=64, topk=64, min_num=20,
+                                                       max_num=300, _idxs=idxs, _keep=keep)
+            np.testing.assert_allclose(mu.cpu().numpy(), g["br_topk_mean"], atol=1e-3, rtol=1e-5)
+        ref = g[f"br_{name}_cov"]
+        np.testing.assert_allclose(cov.cpu().numpy(), ref, rtol=COV_RTOL, atol=1e-4 * np.abs(ref).max())

@@ -172,3 +172,29 @@ def test_demo_cat_pose_from_the_references_evd(device, eu):
                                                         torch.from_numpy(vertex).to(device), mean, _idxs=idxs)
     Rt2 = eu.pose_from_voting(m2, c2, g["points_3d"], K_LM).cpu().numpy()[0]
     np.testing.assert_allclose(Rt2, g["pose"], atol=2e-5)
+
+
+def test_ycb21_pose_from_voting(device, eu):
+    """configs[4] on the device: 21 keypoints, YCB camera, v3 -> EVD with
+    mean -> uncertainty PnP, with the reference's idxs injected.  The
+    reference's own covariances (golden) give the same pose through the
+    device PnP as through the oracle PnP, and the device's voting gives the
+    pose the field was generated from."""
+    from pvnet_amd import ransac_voting_gpu as rvg
+    from tests import golden_io as G
+    g = G.load("ycb21_cases")
+    K, p3 = g["camera"], g["points_3d"]
+    mean = torch.from_numpy(g["v3_keypoints"]).to(device)
+    Rt = eu.pose_from_voting(mean, torch.from_numpy(g["evdm_cov"]).to(device), p3, K).cpu().numpy()[0]
+    ref = P.uncertainty_pnp(g["v3_keypoints"][0], P.weights_from_cov(g["evdm_cov"][0]), p3, K)
+    np.testing.assert_allclose(Rt, ref, atol=1e-6)
+    # noisy field (0.05 rad, 20 % outliers): 0.2 mrad / 6 mm (z at 1 m) from the generating pose
+    np.testing.assert_allclose(Rt, g["pose"], atol=1e-2)
+    mask, vertex, _ = G.ycb_inputs(g)
+    m, v = torch.from_numpy(mask).to(device), torch.from_numpy(vertex).to(device)
+    kp = rvg.ransac_voting_layer_v3(m, v, 512, _idxs=g["v3_idxs"].astype(np.int32))
+    _, cov = rvg.estimate_voting_distribution_with_mean(m, v, kp, _idxs=g["evdm_idxs"].astype(np.int32)
+                                                        .reshape(1, -1, 21, 2))
+    Rt2 = eu.pose_from_voting(kp, cov, p3, K).cpu().numpy()[0]
+    # device keypoints within 1e-2 px and covariances within 1e-4 of the reference's
+    np.testing.assert_allclose(Rt2, ref, atol=1e-4)

@@ -167,3 +167,37 @@ def test_v5_matches_reference_golden():
 def test_motion_voting_matches_reference_golden():
     g = G.load("motion_cases")
     np.testing.assert_allclose(O.ransac_motion_voting(g["mask"], g["vertex"]), g["points"], atol=1e-3, rtol=0)
+
+
+def test_ycb21_v3_and_evd_with_mean():
+    """configs[4] shapes (21 keypoints, YCB camera): v3 bit-exact counts and
+    hypotheses, keypoints; EVD with mean (16 x 256 hypotheses) covariances."""
+    g = G.load("ycb21_cases")
+    mask, vertex, _ = G.ycb_inputs(g)
+    gg = {k[3:]: (g[k].astype(np.int32) if k in ("v3_idxs", "v3_counts") else g[k])
+          for k in g if k.startswith("v3_")}
+    _, diag = check_v3(mask, vertex, gg)
+    assert diag[0]["iters"] == int(g["v3_iters"])
+    _, cov = O.estimate_voting_distribution_with_mean(mask, vertex, g["v3_keypoints"],
+                                                      idxs=[list(g["evdm_idxs"][0].astype(np.int32))])
+    np.testing.assert_allclose(cov, g["evdm_cov"], rtol=COV_RTOL, atol=1e-4 * np.abs(g["evdm_cov"]).max())
+
+
+def test_ycb21_evd_branches():
+    """RV:343-348 (foreground < min_num: zero hypotheses, ratio 1 -> the
+    covariance of the origin about the mean) and RV:351-355 (downsampled,
+    foreground re-counted) in one batch, both EVD variants."""
+    g = G.load("ycb21_cases")
+    keep = lambda name: np.stack([np.ones((40, 48), bool), np.ones((40, 48), bool), g[f"br_{name}_keep2"]])
+    ix = g["br_mean_idxs"]
+    _, cov = O.estimate_voting_distribution_with_mean(
+        g["br_mask"], g["br_vertex"], g["br_mean"], round_hyp_num=32, min_hyp_num=128, max_num=300,
+        idxs=[list(ix[0]), None, list(ix[1])], keep=keep("mean"))
+    np.testing.assert_allclose(cov, g["br_mean_cov"], rtol=COV_RTOL, atol=1e-4 * np.abs(g["br_mean_cov"]).max())
+    assert np.abs(g["br_mean_cov"][1]).max() > 0          # the skipped image's covariance is not zero
+    ix = g["br_topk_idxs"]
+    mu, cov = O.estimate_voting_distribution(
+        g["br_mask"], g["br_vertex"], round_hyp_num=64, min_hyp_num=64, topk=64, min_num=20, max_num=300,
+        idxs=[list(ix[0]), None, list(ix[1])], keep=keep("topk"))
+    np.testing.assert_allclose(mu, g["br_topk_mean"], atol=1e-3, rtol=1e-5)
+    np.testing.assert_allclose(cov, g["br_topk_cov"], rtol=COV_RTOL, atol=1e-4 * np.abs(g["br_topk_cov"]).max())

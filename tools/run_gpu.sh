@@ -15,7 +15,7 @@ step() {  # step <name> <seconds> <cmd...>
 }
 for s in "$@"; do
   case $s in
-    tests) step gpu_tests 900 python -m pytest tests -m gpu -x -q ;;
+    tests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     testsall) step gpu_tests 900 python -m pytest tests -m gpu -q ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
