@@ -34,6 +34,9 @@ HIPCC_FLAGS = [
     # the abs/neg source modifiers the vote test relies on
     "-fno-slp-vectorize",
     "-fno-gpu-rdc",
+    # MFMA results straight into VGPRs (gfx950's unified register file): the
+    # vote kernel's VALU reads them without v_accvgpr_read copies
+    "-mllvm", "-amdgpu-mfma-vgpr-form=1",
     "-Wall",
 ]
 

@@ -56,6 +56,11 @@ __host__ __device__ inline int64_t align_up(int64_t x, int64_t a) { return (x + 
 // exact reference arithmetic (contraction is off for the whole file)
 // --------------------------------------------------------------------------
 
+// KU's guards compare a float against the double 1e-6: (double)x < 1e-6 holds
+// exactly when x <= 1e-6f (the float nearest 1e-6 lies below it), so the
+// guard runs in f32 without the two f64 conversions (NaN: false either way)
+__device__ __forceinline__ bool below_1e6(float x) { return x <= 1e-6f; }
+
 // KU:107-125: one (h, v, t) decision.
 __device__ __forceinline__ bool exact_vote(float nx, float ny, float cx, float cy, float hx, float hy,
                                            float thr) {
@@ -63,7 +68,7 @@ __device__ __forceinline__ bool exact_vote(float nx, float ny, float cx, float c
     float dy = hy - cy;
     float norm1 = sqrtf(nx * nx + ny * ny);
     float norm2 = sqrtf(dx * dx + dy * dy);
-    if ((double)norm1 < 1e-6 || (double)norm2 < 1e-6) return false;
+    if (below_1e6(norm1) || below_1e6(norm2)) return false;
     float angle_dist = (dx * nx + dy * ny) / (norm1 * norm2);
     return angle_dist > thr;
 }
@@ -74,9 +79,9 @@ __device__ __forceinline__ bool exact_intersect(float dx0, float dy0, float cx0,
     float nx0 = dy0, ny0 = -dx0;
     float nx1 = dy1, ny1 = -dx1;
     float d0 = nx1 * ny0 - nx0 * ny1;
-    if ((double)fabsf(d0) < 1e-6) return false;
+    if (below_1e6(fabsf(d0))) return false;
     float d1 = ny1 * nx0 - ny0 * nx1;
-    if ((double)fabsf(d1) < 1e-6) return false;
+    if (below_1e6(fabsf(d1))) return false;
     float p0 = nx0 * cx0 + ny0 * cy0;
     float p1 = nx1 * cx1 + ny1 * cy1;
     *oy = (nx1 * p0 - nx0 * p1) / d0;
@@ -563,7 +568,7 @@ __device__ __forceinline__ float wave_max(float x) { return wave_reduce<true>(x)
 // fast data of one pixel from its raw direction (API path without a prepped array)
 __device__ __forceinline__ float4 prep_pixel(float cx, float cy, float nx, float ny) {
     float n1 = sqrtf(nx * nx + ny * ny);                 // exactly the reference's norm1
-    bool ok = !((double)n1 < 1e-6);
+    bool ok = !below_1e6(n1);
     double N = sqrt((double)nx * nx + (double)ny * ny);
     return make_float4(ok ? cx : __builtin_nanf(""), cy, (float)(nx / N), (float)(ny / N));
 }
@@ -574,7 +579,7 @@ __device__ __forceinline__ float4 prep_pixel(float cx, float cy, float nx, float
 // needs only its direction); *exo: votes, but outside the fast domain
 __device__ __forceinline__ float4 prep_compacted(const F4 &e, bool *exo) {
     const float n1 = sqrtf(e.z * e.z + e.w * e.w);
-    const bool valid = !((double)n1 < 1e-6);
+    const bool valid = !below_1e6(n1);
     const float rs = __builtin_amdgcn_rsqf(fmaf(e.z, e.z, e.w * e.w));
     *exo = valid && !(n1 <= kN1Max);
     return make_float4(valid ? e.x : __builtin_nanf(""), e.y, e.z * rs, e.w * rs);
@@ -582,7 +587,7 @@ __device__ __forceinline__ float4 prep_compacted(const F4 &e, bool *exo) {
 
 __device__ __forceinline__ bool pixel_exotic(float nx, float ny) {
     float n1 = sqrtf(nx * nx + ny * ny);
-    return !((double)n1 < 1e-6) && !(n1 <= kN1Max);     // votes, but outside the fast domain
+    return !below_1e6(n1) && !(n1 <= kN1Max);     // votes, but outside the fast domain
 }
 
 // One segment = pixels [ts, te) of one (image b, keypoint v, hypothesis group
@@ -1114,6 +1119,403 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         a.trace[wave * 8 + 2] = ((uint64_t)xcc << 32) | hw;
         a.trace[wave * 8 + 3] = ((uint64_t)nseg << 32) | (uint32_t)nfix;
         a.trace[wave * 8 + 4] = tloop;
+    }
+}
+
+// ==========================================================================
+// K5m: the fused vote/count on the matrix cores (block-shared layout, hn a
+// multiple of 512).  The rotated-frame test's two forms are linear in the
+// hypothesis:
+//     X = tau (u.h' - u.c') = a_X . h' - b_X,   a_X = tau u
+//     Y =      u x h' - u x c' = a_Y . h' - b_Y,   a_Y = (-u_y, u_x)
+// and z = X - |Y| (= x' tau - |y'| of the VALU kernel above).  One
+// v_mfma_f32_32x32x8_f16 evaluates both forms for 16 pixels x 32 hypotheses
+// (rows = (pixel, form), columns = hypotheses) from hi/lo-split fp16
+// operands, K = 8:
+//     row (pixel form): [ax_hi, ax_hi, ax_lo, ay_hi | ay_hi, ay_lo, -b_hi, -b_lo]
+//     col (hypothesis): [hx_hi, hx_lo, hx_hi, hy_hi | hy_lo, hy_hi,  s,     s   ]
+// (products of fp16 are exact in the f32 accumulation; the lo x lo terms are
+// dropped; s = 2^-k keeps |h' s| < 2^14 in fp16 range).  The VALU is left with
+// z = X - |Y| (one fast-rate v_sub), the sign count (v_perm + v_sad_u8) and
+// the band check (v_minimum3 of |z|): ~18 instructions per 8 pairs per lane
+// instead of ~54 (tools/valu_rates.hip: add/fma/or issue at ~2.7 cycles per
+// wave64 instruction, min/perm/sad at ~4.3).
+//
+// Exactness: the MFMA path's error is bounded by gzm * |a| * B with
+// B >= |h'| + |c'| (fp16 splits, the f32 sums of the
+// matrix core -- measured within 5.2 ulp of sum|terms| on 2M random
+// 16-term sums, tools/mfma_probe.hip, bounded here by 10 --, the rounded
+// h', c', b and tau u); a pair is decided by the fast sign only if
+// |z| > (gzm + gzr) B s (cheap per hypothesis and sub-chunk); the few that
+// are not are re-checked after the sub-chunk against gzm B + gzr D with the
+// pair's own distance D, and decided by the reference's sequence when
+// inside it -- every decision equals KU:116-125's.
+// ==========================================================================
+typedef _Float16 h4f __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kMB = 16;                        // pixels per MFMA batch (32 rows: 16 pixels x (X, Y))
+constexpr int kMBatch = kVoteChunk / kMB;      // batches per sub-chunk (16)
+constexpr int kMSet = 4;                       // 32-hypothesis column sets per wave (128 hypotheses)
+constexpr float kMHypMax = 8.0e6f;             // |hx|, |hy| above -> exact-only (keeps s >= 2^-9)
+constexpr float kMRMax = 30000.f;              // sub-chunk radius above -> exact sub-chunk (fp16 range of b)
+
+template <bool PREPPED>
+struct MSlab {
+    uint4 rows[kMBatch][2 * kMB];              // [batch][row = 2 pixel + form (X, Y)]: k 0..7 as 8 halves (8 KiB)
+    ExactSlab<PREPPED> x;
+};
+
+__device__ __forceinline__ uint32_t pack_h2(_Float16 lo, _Float16 hi) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+}
+
+// a row of the A operand: features of one pixel form (ax, ay, b) as 8 halves
+__device__ __forceinline__ uint4 form_row(float ax, float ay, float b) {
+    const _Float16 axh = (_Float16)ax, axl = (_Float16)(ax - (float)axh);
+    const _Float16 ayh = (_Float16)ay, ayl = (_Float16)(ay - (float)ayh);
+    const float nb = -b;
+    const _Float16 bh = (_Float16)nb, bl = (_Float16)(nb - (float)bh);
+    return make_uint4(pack_h2(axh, axh), pack_h2(axl, ayh), pack_h2(ayh, ayl), pack_h2(bh, bl));
+}
+
+template <bool PREPPED>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_vote_mfma(VoteArgs a) {
+    const int lane = lane_id();
+    const int wid = (int)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int col = lane & 31, half = lane >> 5;
+    const int unit = (int)blockIdx.x;
+    const uint32_t nunits = gridDim.x;
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_setprio(3);
+    __shared__ MSlab<PREPPED> slab[2];
+    __shared__ QuarterBoxes qb_all[2];
+    __shared__ float2 hyp_all[4 * kGroup];     // each wave's 128 exact hypotheses, [set][column]
+    float2 *hlds = hyp_all + wid * kGroup;
+    const int ggn = a.hgn / 4;
+    uint32_t total = 0;
+    for (int b = 0; b < a.b; ++b) total += (uint32_t)(a.vn * ggn) * (uint32_t)(a.tn_dev ? a.tn_dev[b] : a.tn_host);
+    uint32_t lo, hi;
+    if (a.rw[0] > 0 && nunits % 4 == 0) round_share(total, nunits, (uint32_t)unit, a.rw, &lo, &hi);
+    else even_share(total, nunits, (uint32_t)unit, &lo, &hi);
+    int buf = 0, nfix = 0, nseg = 0, nslow = 0, nxo = 0;
+    uint64_t tloop = 0;
+    const float tau = a.tau;
+    constexpr float kBig = 3.0e38f;
+    int b = 0;
+    uint32_t base = 0;
+    while (lo < hi) {
+        const int n = a.tn_dev ? a.tn_dev[b] : a.tn_host;
+        const uint32_t span = (uint32_t)(a.vn * ggn) * (uint32_t)n;
+        if (lo >= base + span) { base += span; ++b; continue; }
+        const uint32_t r0 = lo - base;
+        const int g = (int)(r0 / (uint32_t)n);
+        const int ts = uniform((int)(r0 - (uint32_t)g * n));
+        const int te = uniform((int)min((uint32_t)n, ts + (hi - lo)));
+        const int v = uniform(g / ggn), gg = g - (g / ggn) * ggn;
+        const int hg = uniform(gg * 4 + wid);
+        // ---- segment: pixels [ts, te) of (b, v) against hypotheses hg*128 .. +127 ----
+        auto load_px = [&](int s0, int np) {
+            const int t = wid * kWave + lane;
+            F4 e{0.f, 0.f, 0.f, 0.f};
+            if (t < np) e = pixel_exact<PREPPED>(a, b, v, s0 + t);
+            return e;
+        };
+        F4 L = load_px(ts, min(kVoteChunk, te - ts));
+        // hypotheses: lane makes h = hg*128 + i*64 + lane (i = 0, 1), stored at
+        // [set 2i + half][col] -- the same linear index
+        uint32_t hfm = 0, hxm = 0;              // per set: fast / exact-only (bit j)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int h = hg * kGroup + i * kWave + lane;
+            const bool hl = h < a.nh;
+            const float2 hv = item_hyp<PREPPED, PREPPED>(a, b, v, h, hl, n, PREPPED && ts == 0);
+            hlds[i * kWave + lane] = hv;
+        }
+        __builtin_amdgcn_wave_barrier();
+        float2 hev[kMSet];
+#pragma unroll
+        for (int j = 0; j < kMSet; ++j) {
+            const int h = hg * kGroup + j * 32 + col;
+            const float2 hv = hlds[j * 32 + col];
+            hev[j] = hv;
+            const bool fin = isfinite(hv.x) && isfinite(hv.y);
+            const bool xo = h < a.nh && fin &&
+                            (hyp_exact_only(hv.x, hv.y) || !(fabsf(hv.x) < kMHypMax && fabsf(hv.y) < kMHypMax));
+            hxm |= xo ? 1u << j : 0u;
+            hfm |= (h < a.nh && fin && !xo) ? 1u << j : 0u;
+        }
+        int cnt[kMSet] = {0, 0, 0, 0};
+        if (a.trace && tloop == 0) tloop = __builtin_amdgcn_s_memrealtime();
+        for (int s0 = ts; s0 < te; s0 += kVoteChunk) {
+            const int np = uniform(min(kVoteChunk, te - s0));
+            MSlab<PREPPED> &S = slab[buf];
+            QuarterBoxes &QB = qb_all[buf];
+            buf ^= 1;
+            // ---- stage: one pixel per thread; the origin is the centre of the
+            // sub-chunk's bounding box (block reduce), so |c'| <= R is small ----
+            const int t = wid * kWave + lane;
+            bool exo_p = false;
+            float xl = kBig, xh = -kBig, yq = 0.f;
+            float4 q = make_float4(__builtin_nanf(""), 0.f, 0.f, 0.f);
+            if (t < np) {
+                const F4 e = L;
+                if (PREPPED) q = prep_compacted(e, &exo_p);
+                else { q = prep_pixel(e.x, e.y, e.z, e.w); exo_p = pixel_exotic(e.z, e.w); }
+                S.x.put(t, e);
+                xl = e.x; xh = e.x; yq = q.y;
+            }
+            if (wid * kWave < np) {
+                const float mn = wave_min(xl), mx = wave_max(xh);
+                float yn, yx;
+                if (PREPPED) {
+                    yn = bcast(yq, 0);
+                    yx = bcast(yq, min(kWave - 1, np - 1 - wid * kWave));
+                } else {
+                    const bool in = t < np;
+                    yn = wave_min(in ? yq : kBig);
+                    yx = wave_max(in ? yq : -kBig);
+                }
+                const uint32_t ex = __builtin_amdgcn_ballot_w64(exo_p) != 0;
+                if (lane == 0) { QB.box[wid] = make_float4(mn, mx, yn, yx); QB.exo[wid] = ex; }
+            } else if (lane == 0) {
+                QB.box[wid] = make_float4(kBig, -kBig, kBig, -kBig);
+                QB.exo[wid] = 0;
+            }
+            // next sub-chunk's loads, in flight across the barriers and the hot loop
+            if (s0 + kVoteChunk < te) L = load_px(s0 + kVoteChunk, min(kVoteChunk, te - s0 - kVoteChunk));
+            __syncthreads();
+            float cxl = kBig, cxh = -kBig, cyl = kBig, cyh = -kBig;
+            uint32_t exq = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 Q = QB.box[k];
+                cxl = fminf(cxl, Q.x); cxh = fmaxf(cxh, Q.y);
+                cyl = fminf(cyl, Q.z); cyh = fmaxf(cyh, Q.w);
+                exq |= QB.exo[k];
+            }
+            float ox = floorf(0.5f * cxl + 0.5f * cxh), oy = floorf(0.5f * cyl + 0.5f * cyh);
+            if (!(fabsf(ox) <= 1.6e7f && fabsf(oy) <= 1.6e7f)) { ox = 0.f; oy = 0.f; }
+            const float axr = fmaxf(cxh - ox, ox - cxl), ayr = fmaxf(cyh - oy, oy - cyl);
+            const float R = __builtin_amdgcn_sqrtf(fmaf(axr, axr, ayr * ayr)) * 1.00001f;
+            bool slow = !a.fast || exq != 0 || !(R <= kMRMax);
+            slow = __builtin_amdgcn_readfirstlane(slow);
+            nslow += slow ? 1 : 0;
+            {
+                uint4 rx = make_uint4(0u, 0u, pack_h2((_Float16)0.f, (_Float16)0.f),
+                                      pack_h2((_Float16)(-60000.f), (_Float16)0.f));   // never votes: X = -6e4 s
+                uint4 ry = make_uint4(0u, 0u, 0u, 0u);
+                if (q.x == q.x && !slow) {
+                    const float cx = q.x - ox, cy = q.y - oy;      // exact for pixel centres
+                    const float axX = tau * q.z, ayX = tau * q.w;
+                    rx = form_row(axX, ayX, fmaf(axX, cx, ayX * cy));
+                    ry = form_row(-q.w, q.z, fmaf(-q.w, cx, q.z * cy));
+                }
+                S.rows[t >> 4][2 * (t & 15)] = rx;
+                S.rows[t >> 4][2 * (t & 15) + 1] = ry;
+            }
+            __syncthreads();
+            if (!slow) {
+                // ---- the hypotheses' B fragments and bands for this origin ----
+                h4f bf[kMSet];
+                float gb[kMSet], sc[kMSet], Bh[kMSet];
+#pragma unroll
+                for (int j = 0; j < kMSet; ++j) {
+                    const bool fj = (hfm >> j) & 1u;
+                    const float hx = hev[j].x - ox, hy = hev[j].y - oy;
+                    const float mag = fmaxf(fabsf(hx), fabsf(hy));
+                    const int e = __builtin_amdgcn_frexp_expf(mag);       // mag < 2^e
+                    const int k = fj ? max(0, e - 14) : 0;
+                    const float s = __builtin_ldexpf(1.f, -k);
+                    const float hxs = hx * s, hys = hy * s;               // exact
+                    const _Float16 xh_ = (_Float16)hxs, xl_ = (_Float16)(hxs - (float)xh_);
+                    const _Float16 yh_ = (_Float16)hys, yl_ = (_Float16)(hys - (float)yh_);
+                    const _Float16 sh = (_Float16)s;
+                    h4f f = half ? h4f{yl_, yh_, sh, sh} : h4f{xh_, xl_, xh_, yh_};
+                    if (!fj) f = h4f{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+                    bf[j] = f;
+                    // B >= |h'| + |c'| + 1 (the +1 covers the fp16 subnormal terms)
+                    const float Bv = (__builtin_amdgcn_sqrtf(fmaf(hx, hx, hy * hy)) * 1.00001f + R) * 1.00001f + 1.f;
+                    Bh[j] = Bv;
+                    sc[j] = s;
+                    gb[j] = fj ? (a.gzf + a.gzr) * Bv * s * 1.00001f : -1.f;
+                }
+                uint32_t neg[kMSet] = {0u, 0u, 0u, 0u};
+                uint64_t hitmask = 0;
+#ifdef PVM_ABL_HOT
+                const int nb = 0;
+#else
+                const int nb = (np + kMB - 1) / kMB;
+#endif
+                const uint2 *arow = (const uint2 *)&S.rows[0][0];
+                // the lane's A fragment of batch p: row (col) of the batch's 32
+                // rows (pixel col>>1, form col&1), k half `half`
+                auto afrag = [&](int p) -> h4f {
+                    const uint2 w = arow[(p * kMB * 2 + col) * 2 + half];
+                    return __builtin_bit_cast(h4f, w);
+                };
+                auto zvals = [&](const f32x16 &c, float z[8]) {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) z[q] = c[2 * q] - fabsf(c[2 * q + 1]);
+                };
+                // z of the lane's 8 pairs -> sign count into neg, returns min |z|
+                auto proc = [&](const f32x16 &c, uint32_t &ng) -> float {
+                    float z[8];
+                    zvals(c, z);
+#pragma unroll
+                    for (int q = 0; q < 8; q += 4) {
+                        const uint32_t p01 = __builtin_amdgcn_perm(__float_as_uint(z[q + 1]), __float_as_uint(z[q]), 0x0c0c0b09u);
+                        const uint32_t p23 = __builtin_amdgcn_perm(__float_as_uint(z[q + 3]), __float_as_uint(z[q + 2]), 0x0b090c0cu);
+                        ng = __builtin_amdgcn_sad_u8(p01, p23, ng);
+                    }
+                    float mb = __builtin_elementwise_minimum(__builtin_elementwise_minimum(fabsf(z[0]), fabsf(z[1])), fabsf(z[2]));
+                    mb = __builtin_elementwise_minimum(__builtin_elementwise_minimum(mb, fabsf(z[3])), fabsf(z[4]));
+                    mb = __builtin_elementwise_minimum(__builtin_elementwise_minimum(mb, fabsf(z[5])), fabsf(z[6]));
+                    return __builtin_elementwise_minimum(mb, fabsf(z[7]));
+                };
+                // software pipelined: the next MFMA is in flight while the
+                // previous one's results are processed, the next batch's A
+                // fragment is read one batch ahead, and the band ballots of a
+                // batch are taken together at its end
+                const f32x16 zero = {};
+                h4f A = afrag(0);
+                f32x16 c0 = __builtin_amdgcn_mfma_f32_32x32x8f16(A, bf[0], zero, 0, 0, 0);
+#pragma unroll 1
+                for (int p = 0; p < nb; ++p) {
+                    const h4f An = afrag(min(p + 1, kMBatch - 1));
+                    const f32x16 c1 = __builtin_amdgcn_mfma_f32_32x32x8f16(A, bf[1], zero, 0, 0, 0);
+                    const float m0 = proc(c0, neg[0]);
+                    const f32x16 c2 = __builtin_amdgcn_mfma_f32_32x32x8f16(A, bf[2], zero, 0, 0, 0);
+                    const float m1 = proc(c1, neg[1]);
+                    const f32x16 c3 = __builtin_amdgcn_mfma_f32_32x32x8f16(A, bf[3], zero, 0, 0, 0);
+                    const float m2 = proc(c2, neg[2]);
+                    c0 = __builtin_amdgcn_mfma_f32_32x32x8f16(An, bf[0], zero, 0, 0, 0);   // (unused after the last batch)
+                    const float m3 = proc(c3, neg[3]);
+                    const uint32_t hb = (__builtin_amdgcn_ballot_w64(m0 <= gb[0]) != 0 ? 1u : 0u) |
+                                        (__builtin_amdgcn_ballot_w64(m1 <= gb[1]) != 0 ? 2u : 0u) |
+                                        (__builtin_amdgcn_ballot_w64(m2 <= gb[2]) != 0 ? 4u : 0u) |
+                                        (__builtin_amdgcn_ballot_w64(m3 <= gb[3]) != 0 ? 8u : 0u);
+                    hitmask |= (uint64_t)hb << (p * kMSet);
+                    A = An;
+                }
+                // positives = slots - negatives (padding and never-voting rows are negative)
+#pragma unroll
+                for (int j = 0; j < kMSet; ++j) cnt[j] += ((hfm >> j) & 1u) ? 8 * nb - (int)(neg[j] / 255u) : 0;
+                // ---- band pairs: the same MFMA again (bit-identical); each pair
+                // against its own distance, bounded from the MFMA's own forms:
+                // D = |h - c| <= |x'| + |y'| = |X| / tau + |Y| (scaled by s;
+                // the forms' own errors, < gzm B s, add < 1e-3 of G), and the
+                // reference's sequence inside the band ----
+#ifdef PVM_ABL_FIX
+                nfix += __popcll(hitmask);
+                hitmask = 0;
+#endif
+                const float kx = a.gzr / tau * 1.0001f, ky = a.gzr * 1.0001f;
+                while (hitmask) {
+                    const int bit = __builtin_ctzll(hitmask);
+                    hitmask &= hitmask - 1;
+                    const int p = bit / kMSet, j = bit % kMSet;
+                    ++nfix;
+                    h4f bj = bf[0];
+                    float gBj = Bh[0], sj = sc[0];
+#pragma unroll
+                    for (int k = 1; k < kMSet; ++k)
+                        if (j == k) { bj = bf[k]; gBj = Bh[k]; sj = sc[k]; }
+                    const bool fj = (hfm >> j) & 1u;
+                    const float G = a.gzf * gBj * sj * 1.001f;
+                    const f32x16 c = __builtin_amdgcn_mfma_f32_32x32x8f16(afrag(p), bj, zero, 0, 0, 0);
+                    uint32_t um = 0;
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const float X = c[2 * q], Y = c[2 * q + 1];
+                        const float zq = X - fabsf(Y);
+                        const float g = fmaf(kx, fabsf(X), fmaf(ky, fabsf(Y), G));
+                        um |= (fabsf(zq) <= g) ? 1u << q : 0u;
+                    }
+                    if (!fj) um = 0;
+                    if (__builtin_amdgcn_ballot_w64(um != 0)) {
+                        const float2 hj = hlds[j * 32 + col];
+                        int corr = 0;
+                        // register pair (2q, 2q + 1) = rows 2m, 2m + 1 with
+                        // m = (q & 1) + 4 (q >> 1) + 2 half: pixel m of the batch
+#pragma unroll 1
+                        for (int q = 0; q < 8; ++q) {
+                            const bool u = (um >> q) & 1u && p * kMB + (q & 1) + 4 * (q >> 1) + 2 * half < np;
+                            if (__builtin_amdgcn_ballot_w64(u)) {
+                                const F4 e = S.x.get(p * kMB + (q & 1) + 4 * (q >> 1) + 2 * half);
+                                float X = c[0], Y = c[1];
+#pragma unroll
+                                for (int k = 1; k < 8; ++k)
+                                    if (q == k) { X = c[2 * k]; Y = c[2 * k + 1]; }
+                                const int r = (u && exact_vote(e.z, e.w, e.x, e.y, hj.x, hj.y, a.thr)) ? 1 : 0;
+                                const int f = (u && !signbit(X - fabsf(Y))) ? 1 : 0;
+                                corr += r - f;
+                            }
+                        }
+#pragma unroll
+                        for (int k = 0; k < kMSet; ++k) cnt[k] += j == k ? corr : 0;
+                    }
+                }
+                // exact-only hypotheses (rare): lane = pixel, one hypothesis at a time
+#pragma unroll
+                for (int j = 0; j < kMSet; ++j) {
+                    uint64_t mm = __builtin_amdgcn_ballot_w64(((hxm >> j) & 1u) && half == 0);
+                    nxo += __popcll(mm);
+#ifdef PVM_ABL_XO
+                    mm = 0;
+#endif
+                    while (mm) {
+                        const int l = __builtin_ctzll(mm);
+                        mm &= mm - 1;
+                        const float2 hx2 = hlds[j * 32 + l];
+                        int c = 0;
+#pragma unroll
+                        for (int k = 0; k < kVoteChunk / kWave; ++k) {
+                            const int jj = k * kWave + lane;
+                            bool e = false;
+                            if (jj < np) {
+                                const F4 x = S.x.get(jj);
+                                e = exact_vote(x.z, x.w, x.x, x.y, hx2.x, hx2.y, a.thr);
+                            }
+                            c += __popcll(__builtin_amdgcn_ballot_w64(e));
+                        }
+                        if (lane == l) cnt[j] += c;
+                    }
+                }
+            } else {
+                // every pair through the reference sequence (lane = hypothesis column;
+                // the two lane halves take alternate pixels)
+#pragma unroll 1
+                for (int jj = half; jj < np; jj += 2) {
+                    const F4 e = S.x.get(jj);
+#pragma unroll
+                    for (int j = 0; j < kMSet; ++j)
+                        if ((hfm | hxm) >> j & 1u) cnt[j] += exact_vote(e.z, e.w, e.x, e.y, hev[j].x, hev[j].y, a.thr);
+                }
+            }
+        }
+        // the two lane halves hold the same hypotheses
+        int32_t *cp = a.counts + (int64_t)b * a.cnt_bs + (int64_t)v * a.cnt_v;
+#pragma unroll
+        for (int j = 0; j < kMSet; ++j) {
+            const int tot = cnt[j] + __shfl_xor(cnt[j], 32);
+            const int h = hg * kGroup + j * 32 + col;
+            if (half == 0 && h < a.nh && tot) atomicAdd(&cp[(int64_t)h * a.cnt_h], tot);
+        }
+        lo += te - ts;
+        ++nseg;
+    }
+    if (a.trace && lane == 0) {
+        const int wave = (int)(blockIdx.x * 4 + wid);
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        a.trace[wave * 8] = t_start;
+        a.trace[wave * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+        a.trace[wave * 8 + 2] = ((uint64_t)xcc << 32) | hw;
+        a.trace[wave * 8 + 3] = ((uint64_t)nseg << 32) | (uint32_t)nfix;
+        a.trace[wave * 8 + 4] = tloop;
+        a.trace[wave * 8 + 5] = ((uint64_t)nslow << 32) | (uint32_t)nxo;
     }
 }
 
@@ -1657,7 +2059,7 @@ struct ByteArgs {
 // fast domain.
 __device__ __forceinline__ float4 api_pixel(const float2 c, const float2 d) {
     const float n1 = sqrtf(d.x * d.x + d.y * d.y);
-    const bool ok = !((double)n1 < 1e-6) && n1 == n1 && isfinite(c.x) && isfinite(c.y);
+    const bool ok = !below_1e6(n1) && n1 == n1 && isfinite(c.x) && isfinite(c.y);
     const float rs = __builtin_amdgcn_rsqf(fmaf(d.x, d.x, d.y * d.y));
     float4 q = make_float4(0.f, 0.f, c.x, c.y);
     if (ok)
@@ -2311,7 +2713,7 @@ __global__ __launch_bounds__(256) void k_vote_vp(const float *direct, const floa
     float fx = hx - cx * hz, fy = hy - cy * hz;
     float n1 = sqrtf(ddx * ddx + ddy * ddy);
     float n2 = sqrtf(fx * fx + fy * fy);
-    if ((double)n1 < 1e-6 || (double)n2 < 1e-6) return;
+    if (below_1e6(n1) || below_1e6(n2)) return;
     float ad = (ddx * fx + ddy * fy) / (n1 * n2);
     float vx = fx * ddx, vy = fy * ddy;
     if (vx < 0 || vy < 0) return;
@@ -2364,6 +2766,13 @@ void fast_constants(float thr, VoteArgs *va) {
     }
 }
 
+// The matrix-core vote (k_vote_mfma): its own fast-path constant (DESIGN.md
+// section 5): per form F the error is <= u |a_F| (31.7 + [X] 2 sqrt 2 tau) B
+// (h', c' and b roundings, fp16 splits 12, b split 4, the matrix core's f32
+// sums 10), z = X - |Y| adds u (tau + 1) B:
+//   gzm = 2 (35.5 tau + 32.7) 2^-24 (2x margin);  gzr as above.
+float mfma_gz(float tau) { return (float)(2.0 * (35.5 * (double)tau + 32.7) / 16777216.0 * 1.0001); }
+
 // persistent vote grid: every block resident at once (the occupancy limit of
 // the kernel: LDS slabs, registers), fewer when the work is small (>= ~128
 // pixel steps per wave)
@@ -2398,9 +2807,29 @@ ByteKnobs &byte_knobs() {
 // the vote launch: block-shared staging when the groups come in fours
 // (SH: at most 4 of its 5 resident blocks per CU, which measured faster for
 // one launch and leaves room for a concurrent image's small kernels)
+bool vote_old() {   // PVVOTE_VC_OLD=1: the VALU vote kernel for A/B runs (read once per process)
+    static const bool old = [] { const char *e = getenv("PVVOTE_VC_OLD"); return e && atoi(e) != 0; }();
+    return old;
+}
+
 template <bool PREPPED>
 void launch_vote(const VoteArgs &va, int64_t pixel_steps, hipStream_t s) {
-    if (va.hgn % 4 == 0) {
+    if (va.hgn % 4 == 0 && !vote_old()) {
+        const int grid = vote_grid_steps(pixel_steps, (const void *)k_vote_mfma<PREPPED>, 4);
+        VoteArgs vr = va;
+        vr.gzf = va.fast ? mfma_gz(va.tau) : 0.f;
+        // work weights of the four resident rounds of blocks (round_share;
+        // PVVOTE_VM_RW overrides for A/B runs, read once per process)
+        static const std::array<int, 4> w = [] {
+            // measured (tools/vm_rw.sh, per-SIMD last wave end, p50): even 29.5 us,
+            // 1150/1050/950/850 26.4, 1300/1100/900/700 26.1, 1450/1150/850/550 25.8
+            std::array<int, 4> r{1450, 1150, 850, 550};
+            if (const char *e = getenv("PVVOTE_VM_RW")) sscanf(e, "%d,%d,%d,%d", &r[0], &r[1], &r[2], &r[3]);
+            return r;
+        }();
+        for (int k = 0; k < 4; ++k) vr.rw[k] = grid == 4 * cu_count() && w[0] > 0 ? std::max(w[k], 1) : 0;
+        k_vote_mfma<PREPPED><<<grid, 256, 0, s>>>(vr);
+    } else if (va.hgn % 4 == 0) {
         const int grid = vote_grid_steps(pixel_steps, (const void *)k_vote_count<PREPPED, true>, 4);
         VoteArgs vr = va;
         if (grid == 4 * cu_count()) {

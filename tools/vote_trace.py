@@ -59,6 +59,8 @@ for name, m in (("1 segment", nseg == 1), ("2 segments", nseg == 2), ("3+ segmen
     if m.any():
         print(f"{name:12s} waves {m.sum():5d}  life median {np.median(life[m]):6.2f}  max {life[m].max():6.2f}")
 print("fix steps per wave: median", np.median(nfix), "p90", np.percentile(nfix, 90), "max", nfix.max())
+nslow, nxo = t[:, 5] >> 32, t[:, 5] & 0xffffffff
+print("slow sub-chunks per wave: mean", nslow.mean(), "max", nslow.max(), "| exact-only hypotheses per wave: mean", nxo.mean(), "max", nxo.max())
 order = np.argsort(life)
 for q in (0.1, 0.5, 0.9, 0.99):
     k = order[int(q * (len(order) - 1))]
