@@ -169,6 +169,8 @@ typedef struct pv_pnp_batch {
     const double *K;        /* [3][3] camera matrix, image i at K + i * K_stride */
     int64_t pts3d_stride;   /* elements; 0 = one set shared by the batch */
     int64_t K_stride;       /* elements; 0 = shared */
+    const double *pts2d64;  /* optional f64 [b][pn][2]: used instead of pts2d when non-NULL (the
+                             * reference's cffi path hands float64 points to Ceres, extend_utils.py:80) */
 } pv_pnp_batch;
 
 /* optional device outputs (any may be NULL) */

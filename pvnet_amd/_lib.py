@@ -42,7 +42,7 @@ class V3Diag(ctypes.Structure):
 
 class PnpBatch(ctypes.Structure):
     _fields_ = [("b", c_i32), ("pn", c_i32), ("mode", c_i32), ("pts2d", c_vp), ("wgt", c_vp), ("pts3d", c_vp),
-                ("K", c_vp), ("pts3d_stride", c_i64), ("K_stride", c_i64)]
+                ("K", c_vp), ("pts3d_stride", c_i64), ("K_stride", c_i64), ("pts2d64", c_vp)]
 
 
 class PnpDiag(ctypes.Structure):

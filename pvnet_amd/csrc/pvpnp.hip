@@ -595,8 +595,8 @@ __global__ __launch_bounds__(64) void k_uncertainty_pnp(pv_pnp_batch bt, const d
     double key = 0.0;
     if (active) {
         const int64_t pi = (int64_t)img * pn + lane;
-        pd.x2d = bt.pts2d[pi * 2];
-        pd.y2d = bt.pts2d[pi * 2 + 1];
+        pd.x2d = bt.pts2d64 ? bt.pts2d64[pi * 2] : (double)bt.pts2d[pi * 2];
+        pd.y2d = bt.pts2d64 ? bt.pts2d64[pi * 2 + 1] : (double)bt.pts2d[pi * 2 + 1];
         pd.x3d = P3[lane * 3];
         pd.y3d = P3[lane * 3 + 1];
         pd.z3d = P3[lane * 3 + 2];
@@ -632,8 +632,9 @@ __global__ __launch_bounds__(64) void k_uncertainty_pnp(pv_pnp_batch bt, const d
             for (int k = 0; k < 4; ++k) {
                 const int s = S.sel[k];
                 for (int c = 0; c < 3; ++c) P[k][c] = P3[s * 3 + c];
-                xx[k][0] = bt.pts2d[((int64_t)img * pn + s) * 2];
-                xx[k][1] = bt.pts2d[((int64_t)img * pn + s) * 2 + 1];
+                const int64_t o = ((int64_t)img * pn + s) * 2;
+                xx[k][0] = bt.pts2d64 ? bt.pts2d64[o] : (double)bt.pts2d[o];
+                xx[k][1] = bt.pts2d64 ? bt.pts2d64[o + 1] : (double)bt.pts2d[o + 1];
             }
             double rv[3], tt[3];
             S.ok = p3p_pose(P, xx, cam, rv, tt) ? 1 : 0;
@@ -673,7 +674,7 @@ __global__ __launch_bounds__(64) void k_uncertainty_pnp(pv_pnp_batch bt, const d
 int check_batch(const pv_pnp_batch *bt) {
     if (!bt || bt->b < 0 || bt->pn < 4 || bt->pn > kMaxPts) return PV_EINVAL;
     if (bt->mode != PV_PNP_WEIGHTS && bt->mode != PV_PNP_COV && bt->mode != PV_PNP_COV_V2) return PV_EINVAL;
-    if (bt->b > 0 && (!bt->pts2d || !bt->wgt || !bt->pts3d || !bt->K)) return PV_EINVAL;
+    if (bt->b > 0 && ((!bt->pts2d && !bt->pts2d64) || !bt->wgt || !bt->pts3d || !bt->K)) return PV_EINVAL;
     if (bt->pts3d_stride < 0 || bt->K_stride < 0) return PV_EINVAL;
     return PV_OK;
 }

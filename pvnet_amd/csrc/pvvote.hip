@@ -183,6 +183,7 @@ struct Workspace {
     uint64_t *fgbits;   // [b][nblk][4] foreground ballot of each wave of a k_fg_count block
     float4 *pex;        // [b][vn][P]   exact pixel data (cx, cy, nx, ny): reference operands
     float2 *hyp;        // [b][nh][vn]  (reference layout)
+    float2 *hypv;       // [b][vn][nh]  keypoint-major copy (pre-generated hypotheses)
     int32_t *win;       // [b][vn]
     float *ratio;       // [b][vn]
     double *refpart;    // [b][vn][kRefineNJ][5]
@@ -208,6 +209,7 @@ Workspace carve(void *base, int b, int H, int W, int vn, int nh) {
     w.fgbits = (uint64_t *)take(8 * 4 * b * nblk);
     w.pex = (float4 *)take(16 * b * vn * P);
     w.hyp = (float2 *)take(8 * (int64_t)b * nh * vn);
+    w.hypv = (float2 *)take(8 * (int64_t)b * nh * vn);
     w.win = (int32_t *)take(4 * b * vn);
     w.ratio = (float *)take(4 * b * vn);
     w.refpart = (double *)take(8 * 5 * (int64_t)b * vn * kRefineNJ);
@@ -456,6 +458,7 @@ struct VoteArgs {
     const float2 *raw;          // !PREPPED: raw[b*vn*P + v*raw_v + t*raw_t]
     const float2 *hyp;          // !GEN: hyp[b*hyp_sb + v*hyp_sv + h*hyp_sh]
     float2 *hyp_out;            // GEN: generated hypotheses [b][nh][vn]
+    float2 *hypv_out;           // k_hyp_gen: keypoint-major copy [b][vn][nh]
     int64_t hyp_sb, hyp_sv, hyp_sh;
     float *diag_hyp;            // GEN: optional copy [b][nh][vn][2]
     const int32_t *idxs;        // GEN: pixel pairs [b][nh][vn][2], or nullptr (counter RNG)
@@ -1122,6 +1125,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     }
 }
 
+// Hypotheses once per launch (pipeline, hyp_pregen), one thread per
+// (image, hypothesis, keypoint): the pixel pair (the caller's idxs or the
+// counter RNG, RV:553) and its intersection (KU:11-49), stored in the
+// reference layout and keypoint-major; images without a vote are left alone.
+__global__ __launch_bounds__(256) void k_hyp_gen(VoteArgs a) {
+    const int64_t per = (int64_t)a.nh * a.vn;
+    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= per * a.b) return;
+    const int b = (int)(gid / per);
+    const int r = (int)(gid - b * per);
+    const int h = r / a.vn, v = r - h * a.vn;
+    const int n = a.tn_dev ? a.tn_dev[b] : a.tn_host;
+    if (n > 0) a.hypv_out[((int64_t)b * a.vn + v) * a.nh + h] = item_hyp<true, true>(a, b, v, h, true, n, true);
+}
+
 // ==========================================================================
 // K5m: the fused vote/count on the matrix cores (block-shared layout, hn a
 // multiple of 512).  The rotated-frame test's two forms are linear in the
@@ -1199,7 +1217,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     if (a.rw[0] > 0 && nunits % 4 == 0) round_share(total, nunits, (uint32_t)unit, a.rw, &lo, &hi);
     else even_share(total, nunits, (uint32_t)unit, &lo, &hi);
     int buf = 0, nfix = 0, nseg = 0, nslow = 0, nxo = 0;
-    uint64_t tloop = 0;
+    uint64_t tloop = 0, t_total = 0, t_hyp = 0;
+    if (a.trace) t_total = __builtin_amdgcn_s_memrealtime();
     const float tau = a.tau;
     constexpr float kBig = 3.0e38f;
     int b = 0;
@@ -1229,7 +1248,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         for (int i = 0; i < 2; ++i) {
             const int h = hg * kGroup + i * kWave + lane;
             const bool hl = h < a.nh;
-            const float2 hv = item_hyp<PREPPED, PREPPED>(a, b, v, h, hl, n, PREPPED && ts == 0);
+            // pre-generated (k_hyp_gen, a.hyp keypoint-major) or made here
+            const float2 hv = a.hyp ? item_hyp<false, PREPPED>(a, b, v, h, hl, n, false)
+                                    : item_hyp<PREPPED, PREPPED>(a, b, v, h, hl, n, PREPPED && ts == 0);
             hlds[i * kWave + lane] = hv;
         }
         __builtin_amdgcn_wave_barrier();
@@ -1246,7 +1267,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             hfm |= (h < a.nh && fin && !xo) ? 1u << j : 0u;
         }
         int cnt[kMSet] = {0, 0, 0, 0};
-        if (a.trace && tloop == 0) tloop = __builtin_amdgcn_s_memrealtime();
+        if (a.trace && t_hyp == 0) t_hyp = __builtin_amdgcn_s_memrealtime();
         for (int s0 = ts; s0 < te; s0 += kVoteChunk) {
             const int np = uniform(min(kVoteChunk, te - s0));
             MSlab<PREPPED> &S = slab[buf];
@@ -1378,6 +1399,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                 // fragment is read one batch ahead, and the band ballots of a
                 // batch are taken together at its end
                 const f32x16 zero = {};
+                if (a.trace && tloop == 0) tloop = __builtin_amdgcn_s_memrealtime();
                 h4f A = afrag(0);
                 f32x16 c0 = __builtin_amdgcn_mfma_f32_32x32x8f16(A, bf[0], zero, 0, 0, 0);
 #pragma unroll 1
@@ -1516,6 +1538,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         a.trace[wave * 8 + 3] = ((uint64_t)nseg << 32) | (uint32_t)nfix;
         a.trace[wave * 8 + 4] = tloop;
         a.trace[wave * 8 + 5] = ((uint64_t)nslow << 32) | (uint32_t)nxo;
+        a.trace[wave * 8 + 6] = t_total;
+        a.trace[wave * 8 + 7] = t_hyp;
     }
 }
 
@@ -2812,10 +2836,25 @@ bool vote_old() {   // PVVOTE_VC_OLD=1: the VALU vote kernel for A/B runs (read 
     return old;
 }
 
+// hypotheses by k_hyp_gen before the vote (default; PVVOTE_HYPGEN=0 makes
+// them in the vote kernel's prologue instead, read once per process):
+// measured 34.6k -> 36.6k images/s, vote kernel 35.2 -> 31.8 us (every
+// block of a keypoint otherwise gathers and intersects the same 512 pairs)
+bool hyp_pregen() {
+    static const bool on = [] { const char *e = getenv("PVVOTE_HYPGEN"); return !e || atoi(e) != 0; }();
+    return on;
+}
+
 template <bool PREPPED>
 void launch_vote(const VoteArgs &va, int64_t pixel_steps, hipStream_t s) {
     if (va.hgn % 4 == 0 && !vote_old()) {
-        const int grid = vote_grid_steps(pixel_steps, (const void *)k_vote_mfma<PREPPED>, 4);
+        // blocks per CU of the persistent grid (PVVOTE_VM_BPC for A/B, read once)
+        // 3 (measured, tools/vm_ab.sh, 8 images in flight): 4 -> 36.6k images/s,
+        // 3 -> 40.2k, 2 -> 39.7k: with 3 of the 4 wave slots of every SIMD one
+        // launch leaves room for the next image's blocks, whose prologue
+        // (dependent loads) then overlaps this one's matrix/VALU work
+        static const int bpc = [] { const char *e = getenv("PVVOTE_VM_BPC"); const int v = e ? atoi(e) : 3; return v >= 1 && v <= 4 ? v : 3; }();
+        const int grid = vote_grid_steps(pixel_steps, (const void *)k_vote_mfma<PREPPED>, bpc);
         VoteArgs vr = va;
         vr.gzf = va.fast ? mfma_gz(va.tau) : 0.f;
         // work weights of the four resident rounds of blocks (round_share;
@@ -2954,7 +2993,15 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
     va.trace = g_vote_trace;
     // the vote kernel generates the hypotheses itself (item_hyp in its
     // prologue, overlapped with its first pixel loads) and stores them in
-    // the reference layout; no separate hypothesis launch
+    // the reference layout; by default (hyp_pregen) one k_hyp_gen launch makes
+    // them first and the vote kernel (k_vote_mfma) reads them keypoint-major
+    if (hyp_pregen() && va.hgn % 4 == 0 && !vote_old()) {
+        va.hypv_out = w.hypv;
+        const int64_t nt = (int64_t)b * nh * vn;
+        k_hyp_gen<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(va);
+        if ((r = last())) return r;
+        va.hyp = w.hypv; va.hyp_sb = (int64_t)vn * nh; va.hyp_sv = nh; va.hyp_sh = 1;
+    }
     if (dg.ev_vote_begin) {
         hipError_t e = hipEventRecord((hipEvent_t)dg.ev_vote_begin, s);
         if (e != hipSuccess) return rc(e);
@@ -2970,6 +3017,7 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
         vc.b = nb;
         vc.pex += (int64_t)b0 * vn * P;
         vc.hyp_out += (int64_t)b0 * nh * vn;
+        if (vc.hyp) vc.hyp += (int64_t)b0 * nh * vn;
         if (vc.diag_hyp) vc.diag_hyp += (int64_t)b0 * nh * vn * 2;
         if (vc.idxs) vc.idxs += (int64_t)b0 * nh * vn * 2;
         vc.counts += (int64_t)b0 * va.cnt_bs;

@@ -40,7 +40,9 @@ def uncertainty_pnp_batch(points_2d: torch.Tensor, wgt: torch.Tensor, points_3d,
                           init_rt: torch.Tensor | None = None, diag: dict | None = None) -> torch.Tensor:
     """Batched uncertainty PnP on the device.
 
-    points_2d  f32 [b, pn, 2]   the voted keypoints (e.g. ransac_voting_layer_v3's output)
+    points_2d  [b, pn, 2] the voted keypoints (e.g. ransac_voting_layer_v3's output); float64
+               points are used at full precision (the reference's single-image path passes
+               float64, extend_utils.py:80), anything else as float32
     wgt        mode "cov" / "cov_v2": f32 [b, pn, 2, 2] covariances (estimate_voting_distribution*);
                mode "weights": f64 [b, pn, 3] (wxx, wxy, wyy)
     points_3d  f64 [pn, 3] shared, or [b, pn, 3]
@@ -59,7 +61,7 @@ def uncertainty_pnp_batch(points_2d: torch.Tensor, wgt: torch.Tensor, points_3d,
         raise RuntimeError("points_2d must be [b, pn, 2]")
     if not 4 <= pn <= 64:
         raise RuntimeError("uncertainty_pnp needs 4 <= pn <= 64 points per image")
-    p2 = points_2d.to(torch.float32).contiguous()
+    p2 = points_2d.contiguous() if points_2d.dtype == torch.float64 else points_2d.to(torch.float32).contiguous()
     if mode == "weights":
         w = wgt.to(device=dev, dtype=torch.float64).contiguous()
         if tuple(w.shape) != (b, pn, 3):
@@ -86,7 +88,9 @@ def uncertainty_pnp_batch(points_2d: torch.Tensor, wgt: torch.Tensor, points_3d,
         ks = 9
     else:
         raise RuntimeError("camera_matrix must be [3, 3] or [b, 3, 3]")
-    bt = _lib.PnpBatch(b, pn, _MODES[mode], p2.data_ptr(), w.data_ptr(), p3.data_ptr(), K.data_ptr(), p3s, ks)
+    f64 = p2.dtype == torch.float64
+    bt = _lib.PnpBatch(b, pn, _MODES[mode], None if f64 else p2.data_ptr(), w.data_ptr(), p3.data_ptr(), K.data_ptr(),
+                       p3s, ks, p2.data_ptr() if f64 else None)
     dg = _lib.PnpDiag()
     keep = []
     if diag is not None:
@@ -122,7 +126,7 @@ def _single(points_2d, wgt, points_3d, camera_matrix, mode):
     pn = np.asarray(points_2d).shape[0]
     assert np.asarray(points_3d).shape[0] == pn and pn >= 4          # EU:72
     dev = _device()
-    p2 = torch.from_numpy(np.ascontiguousarray(points_2d, np.float32)).to(dev)[None]
+    p2 = torch.from_numpy(np.ascontiguousarray(points_2d, np.float64)).to(dev)[None]   # EU:80
     w = np.ascontiguousarray(wgt, np.float64 if mode == "weights" else np.float32)
     w = torch.from_numpy(w).to(dev)[None]
     Rt = uncertainty_pnp_batch(p2, w, np.asarray(points_3d, np.float64), np.asarray(camera_matrix, np.float64), mode)

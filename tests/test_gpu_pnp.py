@@ -198,3 +198,20 @@ def test_ycb21_pose_from_voting(device, eu):
     Rt2 = eu.pose_from_voting(kp, cov, p3, K).cpu().numpy()[0]
     # device keypoints within 1e-2 px and covariances within 1e-4 of the reference's
     np.testing.assert_allclose(Rt2, ref, atol=1e-4)
+
+
+def test_float64_image_points_keep_full_precision(device, eu):
+    """The single-image drop-ins take float64 points like the reference's cffi
+    path (extend_utils.py:80): sub-f32 detail reaches the LM, the batched
+    form takes float64 tensors the same way, and float32 still works."""
+    p2, cov, p3, _ = _batch([13])
+    x = p2[0].astype(np.float64) + np.random.default_rng(1).uniform(-3e-5, 3e-5, p2[0].shape)
+    w = P.weights_from_cov(cov[0])
+    Rt = eu.uncertainty_pnp(x, w, p3, K_LM)
+    np.testing.assert_allclose(Rt, P.uncertainty_pnp(x, w, p3, K_LM), atol=TOL)
+    Rb = eu.uncertainty_pnp_batch(torch.from_numpy(x[None]).to(device), torch.from_numpy(w[None]).to(device), p3, K_LM,
+                                  mode="weights").cpu().numpy()[0]
+    np.testing.assert_allclose(Rb, Rt, atol=1e-12)
+    R32 = eu.uncertainty_pnp_batch(torch.from_numpy(x[None].astype(np.float32)).to(device),
+                                   torch.from_numpy(w[None]).to(device), p3, K_LM, mode="weights").cpu().numpy()[0]
+    np.testing.assert_allclose(R32, P.uncertainty_pnp(x.astype(np.float32), w, p3, K_LM), atol=TOL)

@@ -60,6 +60,11 @@ for name, m in (("1 segment", nseg == 1), ("2 segments", nseg == 2), ("3+ segmen
         print(f"{name:12s} waves {m.sum():5d}  life median {np.median(life[m]):6.2f}  max {life[m].max():6.2f}")
 print("fix steps per wave: median", np.median(nfix), "p90", np.percentile(nfix, 90), "max", nfix.max())
 nslow, nxo = t[:, 5] >> 32, t[:, 5] & 0xffffffff
+if (t[:, 6] > 0).all():
+    tt = (t[:, 6] - t0) / 100.0 - s_us
+    th = (t[:, 7] - t0) / 100.0 - s_us
+    print("after the work split (us): p10 %.2f p50 %.2f p90 %.2f" % tuple(np.percentile(tt, [10, 50, 90])))
+    print("after the hypotheses (us): p10 %.2f p50 %.2f p90 %.2f" % tuple(np.percentile(th, [10, 50, 90])))
 print("slow sub-chunks per wave: mean", nslow.mean(), "max", nslow.max(), "| exact-only hypotheses per wave: mean", nxo.mean(), "max", nxo.max())
 order = np.argsort(life)
 for q in (0.1, 0.5, 0.9, 0.99):
