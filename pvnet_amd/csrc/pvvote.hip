@@ -1197,8 +1197,11 @@ __device__ __forceinline__ uint4 form_row(float ax, float ay, float b) {
     return make_uint4(pack_h2(axh, axh), pack_h2(axl, ayh), pack_h2(ayh, ayl), pack_h2(bh, bl));
 }
 
+#ifndef PVM_WPE
+#define PVM_WPE 3   // 152 VGPRs, no spills (4: 128, spilled across the hot loop): 40.4k -> 41.5k images/s
+#endif
 template <bool PREPPED>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_vote_mfma(VoteArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PVM_WPE))) void k_vote_mfma(VoteArgs a) {
     const int lane = lane_id();
     const int wid = (int)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int col = lane & 31, half = lane >> 5;
