@@ -1177,6 +1177,7 @@ constexpr int kMBatch = kVoteChunk / kMB;      // batches per sub-chunk (16)
 constexpr int kMSet = 4;                       // 32-hypothesis column sets per wave (128 hypotheses)
 constexpr float kMHypMax = 8.0e6f;             // |hx|, |hy| above -> exact-only (keeps s >= 2^-9)
 constexpr float kMRMax = 30000.f;              // sub-chunk radius above -> exact sub-chunk (fp16 range of b)
+constexpr int kMQueue = 256;                   // band pairs queued per wave before a reference pass
 
 template <bool PREPPED>
 struct MSlab {
@@ -1212,7 +1213,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
     __shared__ MSlab<PREPPED> slab[2];
     __shared__ QuarterBoxes qb_all[2];
     __shared__ float2 hyp_all[4 * kGroup];     // each wave's 128 exact hypotheses, [set][column]
+    __shared__ uint32_t bq_all[4][kMQueue];     // each wave's band pairs awaiting the reference sequence
+    __shared__ int32_t corr_all[4][kGroup];     // each wave's count corrections, [set][column]
     float2 *hlds = hyp_all + wid * kGroup;
+    uint32_t *bq = bq_all[wid];
+    int32_t *corr = corr_all[wid];
     const int ggn = a.hgn / 4;
     uint32_t total = 0;
     for (int b = 0; b < a.b; ++b) total += (uint32_t)(a.vn * ggn) * (uint32_t)(a.tn_dev ? a.tn_dev[b] : a.tn_host);
@@ -1270,6 +1275,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
             hfm |= (h < a.nh && fin && !xo) ? 1u << j : 0u;
         }
         int cnt[kMSet] = {0, 0, 0, 0};
+        corr[lane] = 0;
+        corr[64 + lane] = 0;
         if (a.trace && t_hyp == 0) t_hyp = __builtin_amdgcn_s_memrealtime();
         for (int s0 = ts; s0 < te; s0 += kVoteChunk) {
             const int np = uniform(min(kVoteChunk, te - s0));
@@ -1436,6 +1443,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                 hitmask = 0;
 #endif
                 const float kx = a.gzr / tau * 1.0001f, ky = a.gzr * 1.0001f;
+                // the queued pairs by the reference's sequence, one pair per lane;
+                // a decision the sign count got wrong corrects (set, column)
+                int nq = 0;
+                auto flush = [&]() {
+                    for (int k0 = 0; k0 < nq; k0 += kWave) {
+                        if (k0 + lane < nq) {
+                            const uint32_t en = bq[k0 + lane];
+                            const int pix = (int)(en & 0xffu), jj = (int)((en >> 8) & 3u), cl = (int)((en >> 10) & 31u);
+                            const int f = (int)(en >> 15) & 1;
+                            const F4 e = S.x.get(pix);
+                            const float2 hj = hlds[jj * 32 + cl];
+                            const int r = exact_vote(e.z, e.w, e.x, e.y, hj.x, hj.y, a.thr) ? 1 : 0;
+                            if (r != f) atomicAdd(&corr[jj * 32 + cl], r - f);
+                        }
+                    }
+                    nq = 0;
+                };
                 while (hitmask) {
                     const int bit = __builtin_ctzll(hitmask);
                     hitmask &= hitmask - 1;
@@ -1449,38 +1473,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                     const bool fj = (hfm >> j) & 1u;
                     const float G = a.gzf * gBj * sj * 1.001f;
                     const f32x16 c = __builtin_amdgcn_mfma_f32_32x32x8f16(afrag(p), bj, zero, 0, 0, 0);
-                    uint32_t um = 0;
+                    // register pair (2q, 2q + 1) = rows 2m, 2m + 1 with
+                    // m = (q & 1) + 4 (q >> 1) + 2 half: pixel m of the batch
 #pragma unroll
                     for (int q = 0; q < 8; ++q) {
                         const float X = c[2 * q], Y = c[2 * q + 1];
                         const float zq = X - fabsf(Y);
                         const float g = fmaf(kx, fabsf(X), fmaf(ky, fabsf(Y), G));
-                        um |= (fabsf(zq) <= g) ? 1u << q : 0u;
-                    }
-                    if (!fj) um = 0;
-                    if (__builtin_amdgcn_ballot_w64(um != 0)) {
-                        const float2 hj = hlds[j * 32 + col];
-                        int corr = 0;
-                        // register pair (2q, 2q + 1) = rows 2m, 2m + 1 with
-                        // m = (q & 1) + 4 (q >> 1) + 2 half: pixel m of the batch
-#pragma unroll 1
-                        for (int q = 0; q < 8; ++q) {
-                            const bool u = (um >> q) & 1u && p * kMB + (q & 1) + 4 * (q >> 1) + 2 * half < np;
-                            if (__builtin_amdgcn_ballot_w64(u)) {
-                                const F4 e = S.x.get(p * kMB + (q & 1) + 4 * (q >> 1) + 2 * half);
-                                float X = c[0], Y = c[1];
-#pragma unroll
-                                for (int k = 1; k < 8; ++k)
-                                    if (q == k) { X = c[2 * k]; Y = c[2 * k + 1]; }
-                                const int r = (u && exact_vote(e.z, e.w, e.x, e.y, hj.x, hj.y, a.thr)) ? 1 : 0;
-                                const int f = (u && !signbit(X - fabsf(Y))) ? 1 : 0;
-                                corr += r - f;
-                            }
+                        const int pix = p * kMB + (q & 1) + 4 * (q >> 1) + 2 * half;
+                        const bool u = fj && pix < np && fabsf(zq) <= g;
+                        const uint64_t m = __builtin_amdgcn_ballot_w64(u);
+                        if (m) {
+                            if (nq > kMQueue - kWave) flush();
+                            const int at = nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                            if (u) bq[at] = (uint32_t)pix | ((uint32_t)j << 8) | ((uint32_t)col << 10) | ((signbit(zq) ? 0u : 1u) << 15);
+                            nq += __popcll(m);
                         }
-#pragma unroll
-                        for (int k = 0; k < kMSet; ++k) cnt[k] += j == k ? corr : 0;
                     }
                 }
+                flush();
+                __builtin_amdgcn_wave_barrier();
                 // exact-only hypotheses (rare): lane = pixel, one hypothesis at a time
 #pragma unroll
                 for (int j = 0; j < kMSet; ++j) {
@@ -1519,7 +1531,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                 }
             }
         }
+        // the reference pass's corrections (LDS atomics of this wave), then
         // the two lane halves hold the same hypotheses
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < kMSet; ++j) cnt[j] += half == 0 ? corr[j * 32 + col] : 0;
         int32_t *cp = a.counts + (int64_t)b * a.cnt_bs + (int64_t)v * a.cnt_v;
 #pragma unroll
         for (int j = 0; j < kMSet; ++j) {
