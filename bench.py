@@ -191,7 +191,7 @@ def main():
 
     # dominant kernels' durations with hipEvents on the streams they run on
     seeds = [rank * 1_000_003 + 17 * k + 3 for k in range(min(K * 5, 100))]
-    vote_ms = time_vote_kernel(rvg, segs, vers, args.hn, seeds, works[0], out_step, s)
+    vote_ms, compact_ms = time_vote_kernel(rvg, segs, vers, args.hn, seeds, works[0], out_step, s)
     # per-image latency: 32 images one after another on one stream (rotating fields)
     NLAT = 32
     lat = torch.cuda.CUDAGraph()
@@ -206,7 +206,8 @@ def main():
     lat.replay()
     torch.cuda.synchronize()
     latency_ms = (time.perf_counter() - t1) / NLAT * 1e3
-    res = dict(elapsed=elapsed, vote_ms=vote_ms, tn=tn, latency_ms=latency_ms, n_images=n_images)
+    res = dict(elapsed=elapsed, vote_ms=vote_ms, compact_ms=compact_ms, tn=tn, latency_ms=latency_ms,
+               n_images=n_images)
     if rank == 0:
         report(args, ws, res, err, dev)
     if ws > 1:
@@ -215,21 +216,26 @@ def main():
 
 
 def time_vote_kernel(rvg, segs, vers, hn, seeds, work, out, stream):
-    """k_vote_count's duration per launch: hipEvents the library records right
-    before and after the vote kernel on the stream it is launched on, over
-    eager calls cycling through the resident fields (events inside a captured
-    graph do not time the nodes between them)."""
+    """Per-launch durations of the vote kernel (k_vote_mfma) and of the
+    compaction (k_fg_count + k_compact): hipEvents the library records right
+    before / after them on the stream they are launched on (the compaction is
+    a call's first work: its start is an event recorded just before the
+    call), over eager calls cycling through the resident fields (events
+    inside a captured graph do not time the nodes between them).
+    Returns (vote ms [n], compaction ms [n])."""
     from pvnet_amd import _lib
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in seeds]
+    ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for _ in seeds]
     with torch.cuda.stream(stream):
-        for a, b in ev:         # materialise the hipEvent_t handles
-            a.record(stream)
-            b.record(stream)
-        for k, (a, b) in enumerate(ev):
-            dd = _lib.V3Diag(ev_vote_begin=a.cuda_event, ev_vote_end=b.cuda_event)
+        for e4 in ev:           # materialise the hipEvent_t handles
+            for e in e4:
+                e.record(stream)
+        torch.cuda.synchronize()
+        for k, (a, b, c0, c1) in enumerate(ev):
+            c0.record(stream)
+            dd = _lib.V3Diag(ev_vote_begin=a.cuda_event, ev_vote_end=b.cuda_event, ev_compact_end=c1.cuda_event)
             _raw_v3(rvg, segs[k % len(segs)], vers[k % len(vers)], hn, seeds[k], work, out[k % out.shape[0]], dd)
     torch.cuda.synchronize()
-    return np.array([a.elapsed_time(b) for a, b in ev])
+    return (np.array([a.elapsed_time(b) for a, b, _, _ in ev]), np.array([c0.elapsed_time(c1) for _, _, c0, c1 in ev]))
 
 
 def _raw_v3(rvg, seg, ver, hn, seed, work, out, dd):
@@ -589,15 +595,30 @@ def report(args, ws, res, final_err, dev):
     pairs = float(args.hn * VN * tn)                # per launch: one launch votes one batch-1 frame
     flops = 12.0 * pairs                            # 12 FLOP per (h,v,t)
     achieved = flops / (vote_ms * 1e-3) / 1e12
-    vc = dict(bound="valu", kernel="k_vote_count (fused vote+count, U2)", achieved=round(achieved, 2),
+    vc = dict(bound="valu", kernel="k_vote_mfma (fused vote+count, U2)", achieved=round(achieved, 2),
               peak=FP32_VECTOR_PEAK_TFLOPS, unit="TFLOP/s", frac=round(achieved / FP32_VECTOR_PEAK_TFLOPS, 4),
-              traffic=pmc_traffic("k_vote_count"), avg_kernel_ms=round(vote_ms, 5), flop_per_launch=flops,
-              note="12 FLOP per (hypothesis, keypoint, pixel) pair (SURVEY 8(d) U2); no inlier mask is "
-                   "materialised, the compulsory bytes are the pixel operands (32 B per pixel and keypoint) and "
-                   "the counts, so the bound is the vector ALU, not HBM or MFMA; traffic = 2*FETCH_SIZE + "
-                   "WRITE_SIZE per launch (%s); avg_kernel_ms from hipEvents the library records around the "
-                   "kernel on its stream in eager calls (rocprof durations of the same run: %s)"
-                   % (PMC_FILE, STATS_FILE))
+              traffic=pmc_traffic("k_vote_mfma"), avg_kernel_ms=round(vote_ms, 5), flop_per_launch=flops,
+              note="12 FLOP per (hypothesis, keypoint, pixel) pair (SURVEY 8(d) U2) against the f32 vector peak; "
+                   "the kernel evaluates the pair's two linear forms on the matrix cores (f16 hi/lo split, "
+                   "v_mfma_f32_32x32x8_f16) and keeps z, the sign count and the guard band on the VALU, which "
+                   "bounds it; no inlier mask is materialised (compulsory bytes: the pixel operands, 16 B per "
+                   "pixel and keypoint, and the counts); traffic = 2*FETCH_SIZE + WRITE_SIZE per launch (%s); "
+                   "avg_kernel_ms from hipEvents the library records around the kernel on its stream in eager "
+                   "calls (rocprof durations of the same run: %s)" % (PMC_FILE, STATS_FILE))
+    # U3: argmax + compaction + strided gather of one frame,
+    # HBM-read bound: H*W*(2 + 2K)*4 B read + tn*(2K + 2)*4 B written
+    comp_ms = float(np.mean(res["compact_ms"]))
+    u3_bytes = H * W * (2 + 2 * VN) * 4 + tn * (2 * VN + 2) * 4
+    u3_gbs = u3_bytes / (comp_ms * 1e-3) / 1e9
+    tc = [pmc_traffic(k) for k in ("k_fg_count", "k_compact")]
+    rc = dict(bound="hbm", kernel="k_fg_count + k_compact (U3: seg_pred argmax, compaction, vertex gather)",
+              achieved=round(u3_gbs, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(u3_gbs / HBM_PEAK_GBS, 4),
+              traffic=None if None in tc else int(sum(tc)), avg_kernel_ms=round(comp_ms, 5),
+              bytes_per_launch=int(u3_bytes),
+              note="algorithmic bytes H*W*(2+2K)*4 + tn*(2K+2)*4 (SURVEY 8(d) U3) / the two kernels' time "
+                   "between an event recorded before the call and the library's ev_compact_end, eager calls "
+                   "(launch gaps included); the pipeline writes 16 B per pixel and keypoint (the reference's "
+                   "(cx, cy, nx, ny) operands), not 8; traffic = the two kernels' PMC bytes (%s)" % PMC_FILE)
     line = {
         "metric": "images/sec (480x640, 9 kp) vote->keypoint",
         "value": round(value, 2),
@@ -624,6 +645,7 @@ def report(args, ws, res, final_err, dev):
                    "images_in_flight": max(1, args.inflight), "stream_images": res["n_images"]},
         "roofline": None,
         "roofline_vote_count": vc,
+        "roofline_compaction": rc,
         "max_kp_err_px": round(final_err, 5),
         "latency_ms_per_image": round(res["latency_ms"], 5),
     }
@@ -632,8 +654,9 @@ def report(args, ws, res, final_err, dev):
     except Exception as e:
         line["kp_err_vs_ref_px"] = {"error": repr(e)}
     # `roofline`: the kernel the north star names, voting_for_hypothesis (U1),
-    # against the HBM peak; the pipeline's own dominant kernel (k_vote_count,
-    # VALU-bound: no inlier mask is materialised) is `roofline_vote_count`
+    # against the HBM peak; the pipeline's own dominant kernel (k_vote_mfma,
+    # VALU-bound: no inlier mask is materialised) is `roofline_vote_count`,
+    # its compaction (U3) `roofline_compaction`
     if not args.skip_u1:
         try:
             u1 = measure_u1(dev, args.hn)

@@ -122,6 +122,8 @@ typedef struct pv_v3_diag {
     float *atb;             /* [b, vn, 2] */
     void *ev_vote_begin;    /* hipEvent_t recorded on `stream` right before / after the fused */
     void *ev_vote_end;      /* vote+count kernel (per-kernel timing in bench.py)                */
+    void *ev_compact_end;   /* hipEvent_t recorded right after the compaction (k_fg_count +
+                             * k_compact, the call's first two kernels)                         */
 } pv_v3_diag;
 
 size_t pv_v3_workspace_size(int32_t b, int32_t H, int32_t W, int32_t vn, int32_t n_hyp);

@@ -37,7 +37,8 @@ class VoteParams(ctypes.Structure):
 
 class V3Diag(ctypes.Structure):
     _fields_ = [("hyp", c_vp), ("counts", c_vp), ("win_idx", c_vp), ("win_ratio", c_vp), ("tn", c_vp),
-                ("iters", c_vp), ("ata", c_vp), ("atb", c_vp), ("ev_vote_begin", c_vp), ("ev_vote_end", c_vp)]
+                ("iters", c_vp), ("ata", c_vp), ("atb", c_vp), ("ev_vote_begin", c_vp), ("ev_vote_end", c_vp),
+                ("ev_compact_end", c_vp)]
 
 
 class PnpBatch(ctypes.Structure):

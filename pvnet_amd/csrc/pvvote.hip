@@ -3000,6 +3000,10 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
     ca.s = s;
     int r = dispatch_mask<CompactStage>(img->mask_kind, evd, (const CompactArgs *)&ca);
     if (r) return r;
+    if (dg.ev_compact_end) {
+        hipError_t e = hipEventRecord((hipEvent_t)dg.ev_compact_end, s);
+        if (e != hipSuccess) return rc(e);
+    }
     VoteArgs va{};
     va.pex = w.pex; va.P = (int32_t)P;
     va.hyp = nullptr;
