@@ -477,9 +477,11 @@ struct VoteArgs {
 // dispatched block runs ahead of its later ones; weighting the earlier
 // rounds more makes the four end together.  Contiguous and exact: unit w
 // starts at total * (B * sum(rw[<r]) + i * rw[r]) / (B * sum(rw)).
+// (rw[3] == 0: three rounds of n / 3 blocks)
 __device__ __forceinline__ void round_share(uint32_t total, uint32_t n, uint32_t w, const int32_t *rw, uint32_t *lo,
                                             uint32_t *hi) {
-    const uint64_t B = n / 4, W = (uint64_t)rw[0] + rw[1] + rw[2] + rw[3];
+    const uint32_t nr = rw[3] > 0 ? 4u : 3u;
+    const uint64_t B = n / nr, W = (uint64_t)rw[0] + rw[1] + rw[2] + rw[3];
     auto pos = [&](uint32_t u) -> uint32_t {
         if (u >= n) return total;
         const uint32_t r = u / (uint32_t)B, i = u % (uint32_t)B;
@@ -1222,7 +1224,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
     uint32_t total = 0;
     for (int b = 0; b < a.b; ++b) total += (uint32_t)(a.vn * ggn) * (uint32_t)(a.tn_dev ? a.tn_dev[b] : a.tn_host);
     uint32_t lo, hi;
-    if (a.rw[0] > 0 && nunits % 4 == 0) round_share(total, nunits, (uint32_t)unit, a.rw, &lo, &hi);
+    if (a.rw[0] > 0 && nunits % (a.rw[3] > 0 ? 4 : 3) == 0) round_share(total, nunits, (uint32_t)unit, a.rw, &lo, &hi);
     else even_share(total, nunits, (uint32_t)unit, &lo, &hi);
     int buf = 0, nfix = 0, nseg = 0, nslow = 0, nxo = 0;
     uint64_t tloop = 0, t_total = 0, t_hyp = 0;
@@ -2885,7 +2887,16 @@ void launch_vote(const VoteArgs &va, int64_t pixel_steps, hipStream_t s) {
             if (const char *e = getenv("PVVOTE_VM_RW")) sscanf(e, "%d,%d,%d,%d", &r[0], &r[1], &r[2], &r[3]);
             return r;
         }();
-        for (int k = 0; k < 4; ++k) vr.rw[k] = grid == 4 * cu_count() && w[0] > 0 ? std::max(w[k], 1) : 0;
+        static const std::array<int, 3> w3 = [] {   // the same for three rounds (PVVOTE_VM_RW3)
+            std::array<int, 3> r{0, 0, 0};
+            if (const char *e = getenv("PVVOTE_VM_RW3")) sscanf(e, "%d,%d,%d", &r[0], &r[1], &r[2]);
+            return r;
+        }();
+        for (int k = 0; k < 4; ++k) vr.rw[k] = 0;
+        if (grid == 4 * cu_count() && w[0] > 0)
+            for (int k = 0; k < 4; ++k) vr.rw[k] = std::max(w[k], 1);
+        else if (grid == 3 * cu_count() && w3[0] > 0)
+            for (int k = 0; k < 3; ++k) vr.rw[k] = std::max(w3[k], 1);
         k_vote_mfma<PREPPED><<<grid, 256, 0, s>>>(vr);
     } else if (va.hgn % 4 == 0) {
         const int grid = vote_grid_steps(pixel_steps, (const void *)k_vote_count<PREPPED, true>, 4);

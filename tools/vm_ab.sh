@@ -1,10 +1,10 @@
 #!/bin/bash
 # A/B of the pipeline's vote variants by environment: GPU parity tests, then
-# the quick bench twice per "name:ENV=VAL,ENV=VAL" spec
+# the quick bench twice per "name:ENV=VAL+ENV=VAL" spec
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 for spec in $SPECS; do
-  name=${spec%%:*}; envs=""; [ "$spec" != "$name" ] && envs=$(echo ${spec#*:} | tr ',' ' ')
+  name=${spec%%:*}; envs=""; [ "$spec" != "$name" ] && envs=$(echo ${spec#*:} | tr '+' ' ')
   if [ -z "$NOTEST" ]; then
     env $envs timeout -k 10 300 python -m pytest tests/test_gpu_parity.py -x -q > gpurun_out/ab_tests_$name.log 2>&1 || { echo "tests failed: $spec"; tail -30 gpurun_out/ab_tests_$name.log; exit 1; }
     echo "$name: $(tail -1 gpurun_out/ab_tests_$name.log)"
