@@ -2852,9 +2852,13 @@ ByteKnobs &byte_knobs() {
 // the vote launch: block-shared staging when the groups come in fours
 // (SH: at most 4 of its 5 resident blocks per CU, which measured faster for
 // one launch and leaves room for a concurrent image's small kernels)
-bool vote_old() {   // PVVOTE_VC_OLD=1: the VALU vote kernel for A/B runs (read once per process)
+// The VALU vote kernel instead of the matrix-core one: PVVOTE_VC_OLD=1 (A/B
+// runs, read once per process) or pv_debug_set_vote_kernel (the tests run
+// both kernels in one process; set between calls, never during a capture)
+int g_vote_kernel = -1;   // -1: environment / default, 0: k_vote_mfma, 1: k_vote_count
+bool vote_old() {
     static const bool old = [] { const char *e = getenv("PVVOTE_VC_OLD"); return e && atoi(e) != 0; }();
-    return old;
+    return g_vote_kernel >= 0 ? g_vote_kernel == 1 : old;
 }
 
 // hypotheses by k_hyp_gen before the vote (default; PVVOTE_HYPGEN=0 makes
@@ -3206,6 +3210,13 @@ int pv_debug_wave_minmax(const float *in, float *out, int32_t nwaves, pv_stream_
 
 // debug only (not in pvvote.h): per-wave timestamps of the next pipeline vote launches
 void pv_debug_set_vote_trace(uint64_t *buf) { g_vote_trace = buf; }
+// debug only (not in pvvote.h): which fused vote/count kernel the pipeline runs
+// (-1 default, 0 matrix-core k_vote_mfma, 1 VALU k_vote_count); returns the previous
+int pv_debug_set_vote_kernel(int32_t which) {
+    const int prev = g_vote_kernel;
+    g_vote_kernel = which < -1 || which > 1 ? -1 : which;
+    return prev;
+}
 // test hook: the byte kernel's debug mode (PVVOTE_DEBUG_BYTES) at run time; returns the previous one
 int pv_debug_set_bytes_mode(int32_t dbg) {
     const int prev = byte_knobs().dbg;

@@ -574,3 +574,36 @@ def test_ycb21_evd_branches(device, rvg):
             np.testing.assert_allclose(mu.cpu().numpy(), g["br_topk_mean"], atol=1e-3, rtol=1e-5)
         ref = g[f"br_{name}_cov"]
         np.testing.assert_allclose(cov.cpu().numpy(), ref, rtol=COV_RTOL, atol=1e-4 * np.abs(ref).max())
+
+
+# ---------------------------------------------------------------- both vote kernels
+@pytest.mark.parametrize("kernel", [0, 1], ids=["k_vote_mfma", "k_vote_count"])
+def test_both_vote_kernels_bit_exact(kernel, device, rvg):
+    """The matrix-core vote kernel (default) and the VALU one give the
+    reference's counts bit for bit: full-size synthetic and cat fields, the
+    edge batch, 21 keypoints, and the EVD rounds (hn 4096) -- selected per
+    call through pv_debug_set_vote_kernel."""
+    import ctypes
+    L = _lib.load()
+    L.pv_debug_set_vote_kernel.argtypes = [ctypes.c_int32]
+    L.pv_debug_set_vote_kernel.restype = ctypes.c_int32
+    prev = L.pv_debug_set_vote_kernel(kernel)
+    try:
+        for name in ("synth_v3_512", "cat_v3_512"):
+            g = G.load(name)
+            mask, vertex = (G.synth_inputs(g) if name.startswith("synth") else G.cat_inputs(g))[:2]
+            run_v3(rvg, mask, vertex, g, "", device)
+        g = G.load("edge_cases")
+        run_v3(rvg, g["c_mask"], g["c_vertex"], g, "c_", device)
+        g = G.load("ycb21_cases")
+        mask, vertex, _ = G.ycb_inputs(g)
+        gg = {k[3:]: (g[k].astype(np.int32) if k in ("v3_idxs", "v3_counts") else g[k])
+              for k in g if k.startswith("v3_")}
+        run_v3(rvg, mask, vertex, gg, "", device)
+        g = G.load("synth_evdm")
+        mask, vertex, _ = G.synth_inputs(g)
+        _, cov = rvg.estimate_voting_distribution_with_mean(cu(mask, device), cu(vertex, device),
+                                                            cu(g["mean"], device), _idxs=g["idxs"][0].reshape(1, -1, 9, 2))
+        np.testing.assert_allclose(cov.cpu().numpy(), g["cov"], rtol=COV_RTOL, atol=1e-4 * np.abs(g["cov"]).max())
+    finally:
+        L.pv_debug_set_vote_kernel(prev)
