@@ -1664,11 +1664,11 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
         if (lane_id() == 0) sacc[threadIdx.x / 64][k] = s;
     }
     __syncthreads();
-    // Two-level hand-off (a single counter would serialise every block's
-    // atomic at one L2 address): the last of the kRefineNJ blocks of (b, v)
-    // sums their partials, the last keypoint of image b solves.
+    // Hand-off: every block publishes its partials and takes a ticket of its
+    // image; the image's last block sums each keypoint's kRefineNJ partials
+    // (in a fixed order: deterministic) and solves them all.  (A ticket per
+    // keypoint and then per image took two more memory round trips.)
     int32_t *tk_img = ticket + (int64_t)b * (1 + vn);
-    int32_t *tk_v = tk_img + 1 + v;
     if (threadIdx.x < 64) {   // wave 0: publish this block's partials, then take a ticket
         const int k = threadIdx.x;
         double *rp = refpart + (((int64_t)b * vn + v) * kRefineNJ + j) * 5;
@@ -1679,39 +1679,37 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         int t = 0;
-        if (k == 0) t = __hip_atomic_fetch_add(tk_v, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == 0) t = __hip_atomic_fetch_add(tk_img, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         t = __shfl(t, 0);
-        if (k == 0) slast = (t == kRefineNJ - 1);
+        if (k == 0) slast = (t == vn * kRefineNJ - 1);
     }
     __syncthreads();
-    if (!slast || threadIdx.x >= 64) return;
-    // ---- last block of (b, v): sum the keypoint's partials (lane = (jj, k)) ----
-    {
-        const int k = threadIdx.x;
-        const double *rp = refpart + ((int64_t)b * vn + v) * kRefineNJ * 5;
+    if (!slast) return;
+    // ---- last block of image b: each keypoint's sums (wave w: keypoints w, w + 4, ...) ----
+    __shared__ double sks[64][5];
+    for (int vv = (int)(threadIdx.x / 64); vv < vn; vv += 4) {
+        const int k = lane_id();
+        const double *rp = refpart + ((int64_t)b * vn + vv) * kRefineNJ * 5;
         double s5[5] = {0, 0, 0, 0, 0};
         for (int jj = k; jj < kRefineNJ; jj += 64)
 #pragma unroll
             for (int q = 0; q < 5; ++q) s5[q] += ld_agent(&rp[jj * 5 + q]);
 #pragma unroll
         for (int q = 0; q < 5; ++q) s5[q] = wave_sum_d(s5[q]);
-        double *ks = ksum + ((int64_t)b * vn + v) * 5;
-        if (k < 5) st_agent(&ks[k], k == 0 ? s5[0] : k == 1 ? s5[1] : k == 2 ? s5[2] : k == 3 ? s5[3] : s5[4]);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        int t = 0;
-        if (k == 0) t = __hip_atomic_fetch_add(tk_img, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        t = __shfl(t, 0);
-        if (t != vn - 1) return;
+        if (k == 0)
+#pragma unroll
+            for (int q = 0; q < 5; ++q) sks[vv][q] = s5[q];
     }
+    __syncthreads();
+    if (threadIdx.x >= 64) return;
     // ---- last keypoint of image b: solve for every keypoint (lane = keypoint) ----
     const int vv = threadIdx.x;
     const bool act = vv < vn;
     float A00 = 0, A01 = 0, A11 = 0, B0 = 0, B1 = 0, rat = 3.0e38f;
     int wi = 0;
     if (act) {
-        const double *ks = ksum + ((int64_t)b * vn + vv) * 5;
-        A00 = (float)ld_agent(&ks[0]); A01 = (float)ld_agent(&ks[1]); A11 = (float)ld_agent(&ks[2]);
-        B0 = (float)ld_agent(&ks[3]); B1 = (float)ld_agent(&ks[4]);
+        A00 = (float)sks[vv][0]; A01 = (float)sks[vv][1]; A11 = (float)sks[vv][2];
+        B0 = (float)sks[vv][3]; B1 = (float)sks[vv][4];
         rat = ld_agent(&ratio_out[b * vn + vv]);
         wi = ld_agent(&win_out[b * vn + vv]);
     }
