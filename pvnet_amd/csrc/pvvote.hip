@@ -1607,19 +1607,21 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
     __shared__ int slast;
     // this block's pixels, loaded before the argmax so both latencies overlap
     constexpr int U = 4;
+    // (guarded by the buffer's extent P, not by tn: the loads do not wait for
+    // tn's; records at t >= tn are read but never used)
     const float4 *eb = pex + ((int64_t)b * vn + v) * P;
     const int t0 = j * 256 + threadIdx.x, tstep = kRefineNJ * 256;
     float4 e[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int t = t0 + u * tstep;
-        e[u] = t < n ? eb[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+        e[u] = t < P ? eb[t] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     // the keypoint's hypotheses too (the winner's is then read from LDS, not
     // fetched after the argmax: one memory round trip fewer)
     constexpr int kRefineLdsHyp = 1024;
     __shared__ float2 shyp[kRefineLdsHyp];
-    if (nh <= kRefineLdsHyp && n > 0)
+    if (nh <= kRefineLdsHyp)
         for (int h = threadIdx.x; h < nh; h += 256) shyp[h] = hyp[((int64_t)b * nh + h) * vn + v];
     // argmax over h, first index on ties: key = count << 32 | ~h
     uint64_t key = 0;
@@ -1685,24 +1687,44 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
     }
     __syncthreads();
     if (!slast) return;
-    // ---- last block of image b: each keypoint's sums (wave w: keypoints w, w + 4, ...) ----
+    // ---- last block of image b: each keypoint's kRefineNJ partials (32 consecutive
+    // records = one half-wave) summed by a fixed shuffle tree, and the keypoints'
+    // winners and ratios, all loads in flight together ----
+    static_assert(kRefineNJ == 32, "a keypoint's partials fill one half-wave");
     __shared__ double sks[64][5];
-    for (int vv = (int)(threadIdx.x / 64); vv < vn; vv += 4) {
-        const int k = lane_id();
-        const double *rp = refpart + ((int64_t)b * vn + vv) * kRefineNJ * 5;
-        double s5[5] = {0, 0, 0, 0, 0};
-        for (int jj = k; jj < kRefineNJ; jj += 64)
+    __shared__ float srat[64];
+    __shared__ int swin[64];
+    {
+        const double *rp = refpart + (int64_t)b * vn * kRefineNJ * 5;
+        const int nrec = vn * kRefineNJ;
+        constexpr int R = 2;                  // rounds in flight together (vn <= 16: all of them)
+        for (int r0 = 0; r0 < nrec; r0 += R * 256) {
+            double s5[R][5];
 #pragma unroll
-            for (int q = 0; q < 5; ++q) s5[q] += ld_agent(&rp[jj * 5 + q]);
+            for (int r = 0; r < R; ++r) {
+                const int i = r0 + r * 256 + (int)threadIdx.x;
 #pragma unroll
-        for (int q = 0; q < 5; ++q) s5[q] = wave_sum_d(s5[q]);
-        if (k == 0)
+                for (int q = 0; q < 5; ++q) s5[r][q] = i < nrec ? ld_agent(&rp[i * 5 + q]) : 0.0;
+            }
+            if (r0 == 0 && threadIdx.x < (unsigned)vn) {
+                srat[threadIdx.x] = ld_agent(&ratio_out[b * vn + threadIdx.x]);
+                swin[threadIdx.x] = ld_agent(&win_out[b * vn + threadIdx.x]);
+            }
 #pragma unroll
-            for (int q = 0; q < 5; ++q) sks[vv][q] = s5[q];
+            for (int r = 0; r < R; ++r) {
+                const int i = r0 + r * 256 + (int)threadIdx.x;
+#pragma unroll
+                for (int q = 0; q < 5; ++q)
+                    for (int o = 16; o > 0; o >>= 1) s5[r][q] += __shfl_xor(s5[r][q], o);
+                if ((lane_id() & 31) == 0 && i < nrec)
+#pragma unroll
+                    for (int q = 0; q < 5; ++q) sks[i / kRefineNJ][q] = s5[r][q];
+            }
+        }
     }
     __syncthreads();
     if (threadIdx.x >= 64) return;
-    // ---- last keypoint of image b: solve for every keypoint (lane = keypoint) ----
+    // ---- solve for every keypoint (lane = keypoint) ----
     const int vv = threadIdx.x;
     const bool act = vv < vn;
     float A00 = 0, A01 = 0, A11 = 0, B0 = 0, B1 = 0, rat = 3.0e38f;
@@ -1710,8 +1732,8 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
     if (act) {
         A00 = (float)sks[vv][0]; A01 = (float)sks[vv][1]; A11 = (float)sks[vv][2];
         B0 = (float)sks[vv][3]; B1 = (float)sks[vv][4];
-        rat = ld_agent(&ratio_out[b * vn + vv]);
-        wi = ld_agent(&win_out[b * vn + vv]);
+        rat = srat[vv];
+        wi = swin[vv];
     }
     float inv[4] = {1.f, 0.f, 0.f, 1.f};
     bool ok = act ? lu2_inv(A00, A01, A01, A11, inv) : true;

@@ -15,7 +15,7 @@ L.pv_debug_compact_trace.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int
 f = synth.synthetic_field(1234)
 seg = torch.from_numpy(f["seg"]).cuda()
 vert = torch.from_numpy(f["vertex"]).cuda()
-for it in range(3):
+for it in range(int(sys.argv[1]) if len(sys.argv) > 1 else 400):
     ransac_voting_layer_v3_from_network(seg, vert, 512)
 torch.cuda.synchronize()
 L.pv_debug_compact_trace(1, None, 0)

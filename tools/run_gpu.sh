@@ -17,6 +17,10 @@ for s in "$@"; do
   case $s in
     tests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     testsall) step gpu_tests 900 python -m pytest tests -m gpu -q ;;
+    lat) step lat 120 python3 tools/lat_trace.py 20 &&
+         step latprof 200 rocprofv3 --kernel-trace -T --output-format csv -d "$PWD/gpurun_out/prof_lat" -o lat -- python3 tools/lat_trace.py 10 &&
+         python3 tools/lat_trace.py --gaps gpurun_out/prof_lat/lat_kernel_trace.csv > gpurun_out/lat_gaps.log 2>&1; cat gpurun_out/lat_gaps.log ;;
+    ctrace) step ctrace 120 python3 tools/compact_trace.py ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     benchfull) step bench 600 python bench.py && cp gpurun_out/bench.log gpurun_out/bench_full.log ;;

@@ -17,11 +17,16 @@ f = synth.synthetic_field(1234)
 seg = torch.from_numpy(f["seg"]).cuda()
 vert = torch.from_numpy(f["vertex"]).cuda()
 buf = torch.zeros(16384 * 8, dtype=torch.int64, device="cuda")
-for it in range(4):
-    buf.zero_()
-    L.pv_debug_set_vote_trace(ctypes.c_void_p(buf.data_ptr()) if it else None)
+# warm clocks: many back-to-back calls without a sync, then the traced call
+WARM = int(sys.argv[1]) if len(sys.argv) > 1 else 400
+L.pv_debug_set_vote_trace(None)
+for it in range(WARM):
     ransac_voting_layer_v3_from_network(seg, vert, 512)
-    torch.cuda.synchronize()
+buf.zero_()
+L.pv_debug_set_vote_trace(ctypes.c_void_p(buf.data_ptr()))
+ransac_voting_layer_v3_from_network(seg, vert, 512)
+torch.cuda.synchronize()
+L.pv_debug_set_vote_trace(None)
 t = buf.view(-1, 8).cpu().numpy()
 t = t[t[:, 0] > 0]
 s, e, hw = t[:, 0], t[:, 1], t[:, 2]
