@@ -217,7 +217,7 @@ def main():
 
 def time_vote_kernel(rvg, segs, vers, hn, seeds, work, out, stream):
     """Per-launch durations of the vote kernel (k_vote_mfma) and of the
-    compaction (k_compact): hipEvents the library records right
+    compaction (k_fg_count + k_compact): hipEvents the library records right
     before / after them on the stream they are launched on (the compaction is
     a call's first work: its start is an event recorded just before the
     call), over eager calls cycling through the resident fields (events
@@ -249,7 +249,7 @@ def _raw_v3(rvg, seg, ver, hn, seed, work, out, dd):
     L = _lib.load()
     nbytes = L.pv_v3_workspace_size(b, h, w, c // 2, hn)
     wsb = work.get(ver.device, nbytes)
-    code = L.pv_ransac_voting_v3(ctypes.byref(d), ctypes.byref(prm), out.data_ptr(), wsb.data_ptr(), wsb.numel(),
+    code = L.pv_ransac_voting_v3(ctypes.byref(d), ctypes.byref(prm), out.data_ptr(), wsb.data_ptr(), nbytes,
                                  ctypes.byref(dd), torch.cuda.current_stream(ver.device).cuda_stream)
     _lib.check(code, "pv_ransac_voting_v3")
     return out
@@ -610,16 +610,15 @@ def report(args, ws, res, final_err, dev):
     comp_ms = float(np.mean(res["compact_ms"]))
     u3_bytes = H * W * (2 + 2 * VN) * 4 + tn * (2 * VN + 2) * 4
     u3_gbs = u3_bytes / (comp_ms * 1e-3) / 1e9
-    tc = [pmc_traffic(k) for k in ("k_compact",)]
-    rc = dict(bound="hbm", kernel="k_compact (U3: seg_pred argmax, single-pass compaction, vertex gather)",
+    tc = [pmc_traffic(k) for k in ("k_fg_count", "k_compact")]
+    rc = dict(bound="hbm", kernel="k_fg_count + k_compact (U3: seg_pred argmax, compaction, vertex gather)",
               achieved=round(u3_gbs, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(u3_gbs / HBM_PEAK_GBS, 4),
               traffic=None if None in tc else int(sum(tc)), avg_kernel_ms=round(comp_ms, 5),
               bytes_per_launch=int(u3_bytes),
-              note="algorithmic bytes H*W*(2+2K)*4 + tn*(2K+2)*4 (SURVEY 8(d) U3) / the kernel's time "
+              note="algorithmic bytes H*W*(2+2K)*4 + tn*(2K+2)*4 (SURVEY 8(d) U3) / the two kernels' time "
                    "between an event recorded before the call and the library's ev_compact_end, eager calls "
-                   "(launch gap included; the fields have fg < max_num, so k_dsample_hyp's downsampling pass "
-                   "has nothing to do); the pipeline writes 16 B per pixel and keypoint (the reference's "
-                   "(cx, cy, nx, ny) operands), not 8; traffic = the kernel's PMC bytes (%s)" % PMC_FILE)
+                   "(launch gaps included); the pipeline writes 16 B per pixel and keypoint (the reference's "
+                   "(cx, cy, nx, ny) operands), not 8; traffic = the two kernels' PMC bytes (%s)" % PMC_FILE)
     line = {
         "metric": "images/sec (480x640, 9 kp) vote->keypoint",
         "value": round(value, 2),

@@ -172,17 +172,15 @@ __device__ __forceinline__ bool is_fg(const MaskView &m, int b, int r, int c) {
 // workspace
 // --------------------------------------------------------------------------
 struct Workspace {
-    int32_t *counts;    // [b][vn][nh]   zeroed by k_compact
-    int32_t *ticket;    // [b][1 + vn]   zeroed by k_compact: per image, per (image, keypoint)
-    int32_t *dsagg;     // [b][nblk]     zeroed by k_compact: downsampled count + 1 per super-block (look-back)
-    int32_t *confc;     // [b][vn][2]    zeroed by k_compact: v5 confidence count, ticket
-    int32_t *dsdone;    // [b]           zeroed by k_compact: downsampling super-blocks done
-    int64_t zero_words; // counts + ticket + dsagg + confc + dsdone (contiguous)
-    int32_t *lbflag;    // [b][nblk]     k_compact's look-back (count + 1); zero between calls (k_dsample_hyp)
-    int64_t flag_bytes; // bytes of lbflag this shape uses (<= flag_region(workspace bytes))
+    int32_t *counts;    // [b][vn][nh]   zeroed by k_fg_count
+    int32_t *ticket;    // [b][1 + vn]   zeroed by k_fg_count: per image, per (image, keypoint)
+    int32_t *dsagg;     // [b][nblk]     zeroed by k_fg_count: downsampled count + 1 per block (look-back)
+    int32_t *confc;     // [b][vn][2]    zeroed by k_fg_count: v5 confidence count, ticket
+    int64_t zero_words; // counts + ticket + dsagg + confc (contiguous)
     int32_t *tn;        // [b] compacted pixels (0 = image skipped)
     int32_t *fgtot;     // [b] foreground before downsampling
-    uint64_t *fgbits;   // [b][nblk][4] foreground ballot of each wave of a k_compact block
+    int32_t *blkcnt;    // [b][nblk]
+    uint64_t *fgbits;   // [b][nblk][4] foreground ballot of each wave of a k_fg_count block
     float4 *pex;        // [b][vn][P]   exact pixel data (cx, cy, nx, ny): reference operands
     float2 *hyp;        // [b][nh][vn]  (reference layout)
     float2 *hypv;       // [b][vn][nh]  keypoint-major copy (pre-generated hypotheses)
@@ -193,31 +191,21 @@ struct Workspace {
     size_t total;
 };
 
-// k_compact's look-back flags must read zero when a call starts.  They live
-// in a region at the start of the workspace whose size depends only on the
-// workspace's byte count (flag_region), and nothing else is ever stored
-// there: a workspace zero-filled once and passed with the same byte count on
-// every call (pvvote.h) keeps the region zero across calls of any shape, as
-// every call returns the flags it used to zero (k_dsample_hyp).
-int64_t flag_region(size_t bytes) { return (int64_t)(bytes / 256) & ~(int64_t)255; }
-
-Workspace carve(void *base, size_t bytes, int b, int H, int W, int vn, int nh) {
+Workspace carve(void *base, int b, int H, int W, int vn, int nh) {
     Workspace w{};
     int64_t P = (int64_t)H * W;
     int64_t nblk = (P + kCompactChunk - 1) / kCompactChunk;
     char *p = (char *)base;
-    int64_t off = flag_region(bytes);
+    int64_t off = 0;
     auto take = [&](int64_t bytes) { char *q = p ? p + off : nullptr; off = align_up(off + bytes, 256); return q; };
-    w.lbflag = (int32_t *)p;
-    w.flag_bytes = 4 * b * nblk;
-    w.zero_words = (int64_t)b * vn * nh + (int64_t)b * (1 + vn) + b * nblk + 2 * (int64_t)b * vn + b;
+    w.zero_words = (int64_t)b * vn * nh + (int64_t)b * (1 + vn) + b * nblk + 2 * (int64_t)b * vn;
     w.counts = (int32_t *)take(4 * w.zero_words);
     w.ticket = w.counts ? w.counts + (int64_t)b * vn * nh : nullptr;
     w.dsagg = w.counts ? w.ticket + (int64_t)b * (1 + vn) : nullptr;
     w.confc = w.counts ? w.dsagg + b * nblk : nullptr;
-    w.dsdone = w.counts ? w.confc + 2 * (int64_t)b * vn : nullptr;
     w.tn = (int32_t *)take(4 * b);
     w.fgtot = (int32_t *)take(4 * b);
+    w.blkcnt = (int32_t *)take(4 * b * nblk);
     w.fgbits = (uint64_t *)take(8 * 4 * b * nblk);
     w.pex = (float4 *)take(16 * b * vn * P);
     w.hyp = (float2 *)take(8 * (int64_t)b * nh * vn);
@@ -228,11 +216,6 @@ Workspace carve(void *base, size_t bytes, int b, int H, int W, int vn, int nh) {
     w.ksum = (double *)take(8 * 5 * (int64_t)b * vn);
     w.total = (size_t)off;
     return w;
-}
-
-// the workspace fits this shape: its flag region holds the shape's flags and the rest follows it
-bool ws_fits(const Workspace &w, const void *base, size_t bytes) {
-    return base && flag_region(bytes) >= w.flag_bytes && w.total <= bytes;
 }
 
 // agent-scope (device-wide) relaxed atomics for the in-kernel hand-offs
@@ -263,19 +246,46 @@ __device__ __forceinline__ int2 block_sum2(int x, int y, int *sh) {
 }
 
 // ==========================================================================
-// K1: single-pass stream compaction (RV:537-552): the foreground test, the
-// row-major rank by decoupled look-back, and the vertex gather; one pixel per
-// thread, 256 per block.  A block publishes its foreground count (+1; 0 = not
-// yet) as soon as its mask is read, issues its pixels' vertex loads, and adds
-// up the counts of the blocks before it.  Dispatch order is not relied on: a
-// count not seen within kLookbackSpin (a block not scheduled yet) is counted
-// from the mask by the waiting thread itself, so every wait ends.  The
-// image's last block writes fgtot and tn -- unless fg > max_num, when the
-// downsampling pass (k_dsample_hyp) writes tn.  Every foreground pixel's
-// records are written either way (tn = 0 hides them when fg < min_num).
-// The look-back flags are returned to zero by k_dsample_hyp (the workspace
-// starts zero-filled: pvvote.h); this kernel zeroes the later kernels'
-// counters.
+// K1: foreground count per 256-pixel block (one pixel per thread) and the
+// block's four wave ballots (k_compact reads 32 B instead of the mask again);
+// zeroes the pipeline's counters
+// ==========================================================================
+template <int KIND, bool EVD>
+__global__ __launch_bounds__(256) void k_fg_count(MaskView m, int H, int W, int32_t *blkcnt, uint64_t *fgbits,
+                                                  int nblk, int32_t *zero, int64_t zero_words) {
+    static_assert(kCompactChunk == 256, "one pixel per thread");
+    const int b = blockIdx.y, blk = blockIdx.x;
+    const int64_t P = (int64_t)H * W;
+    {   // zero counts + tickets (read only by later kernels of this pipeline)
+        int64_t g = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x;
+        int64_t G = (int64_t)gridDim.x * gridDim.y * 256;
+        for (int64_t i = g; i < zero_words; i += G) zero[i] = 0;
+    }
+    __shared__ int sh[8];
+    const int64_t p = (int64_t)blk * kCompactChunk + threadIdx.x;
+    const bool f = p < P && is_fg<KIND, EVD>(m, b, (int)((uint32_t)p / (uint32_t)W), (int)((uint32_t)p % (uint32_t)W));
+    const uint64_t bal = ballot(f);
+    if (lane_id() == 0) fgbits[((int64_t)b * nblk + blk) * 4 + threadIdx.x / 64] = bal;
+    int2 t = block_sum2(f ? 1 : 0, 0, sh);
+    if (threadIdx.x == 0) blkcnt[b * nblk + blk] = t.x;
+}
+
+// foreground total of image b from the per-block counts (every block of K1b/K2 does this)
+__device__ __forceinline__ int2 image_totals(const int32_t *cnt, int nblk, int upto, int *sh) {
+    int all = 0, pre = 0;
+    for (int j = threadIdx.x; j < nblk; j += 256) {
+        int v = cnt[j];
+        all += v;
+        pre += j < upto ? v : 0;
+    }
+    return block_sum2(all, pre, sh);
+}
+
+// ==========================================================================
+// K2: row-major stream compaction (RV:548-552): coords (x=col, y=row) and the
+// per-keypoint raw directions, keypoint-major so the vote waves read them
+// contiguously.  Reads the [b,H,W,vn,2] view through its strides, so the
+// network's NCHW vertex_pred is gathered directly (no permute copy).
 // ==========================================================================
 // debug-only phase stamps (s_memrealtime) of the compaction blocks; see
 // pv_debug_compact_trace
@@ -285,8 +295,6 @@ __device__ __forceinline__ void cstamp(int blk, int k) {
     if (g_ctrace_on && threadIdx.x == 0 && blk < 4096) g_ctrace[blk * 4 + k] = __builtin_amdgcn_s_memrealtime();
 }
 
-constexpr uint64_t kLookbackSpin = 20000;   // s_memrealtime ticks (100 MHz): 200 us
-
 struct VertexView {
     const void *p;
     int kind;
@@ -295,84 +303,14 @@ struct VertexView {
 };
 
 constexpr int kCompactKp = 12;   // keypoints whose vertex loads a compaction thread keeps in flight at once
-
-// One pixel's vertex loads: buffer loads through a per-image descriptor, one
-// VGPR offset for the pixel and the keypoint / component plane offsets in
-// SGPRs (host check: the image's view spans < 2 GiB); a group of kCompactKp
-// keypoints in flight together.
-template <int VK>
-struct VertexGather {
-    __amdgpu_buffer_rsrc_t rsrc;
-    int voff, vn, so_v, so_c;
-    float nx[kCompactKp], ny[kCompactKp];
-    __device__ __forceinline__ VertexGather(const VertexView &vx, int b, int r, int c, int vn_) {
-        constexpr int ES = VK == PV_VERTEX_F32 ? 4 : 2;
-        rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)((const char *)vx.p + (int64_t)b * vx.s[0] * ES), (short)0,
-                                                 vx.extent, 0x00020000);
-        voff = (int)((r * vx.s[1] + c * vx.s[2]) * ES);
-        vn = vn_;
-        so_v = (int)(vx.s[3] * ES);
-        so_c = (int)(vx.s[4] * ES);
-    }
-    __device__ __forceinline__ void load(int v0, bool f) {
-#pragma unroll
-        for (int u = 0; u < kCompactKp; ++u) {
-            nx[u] = ny[u] = 0.f;
-            if (f && v0 + u < vn) {
-                const int so = uniform((v0 + u) * so_v);
-                const int s4 = uniform(so_c);
-                if constexpr (VK == PV_VERTEX_F32) {
-                    nx[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, so, 0));
-                    ny[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, so + s4, 0));
-                } else {
-                    nx[u] = __half2float(__ushort_as_half(__builtin_amdgcn_raw_buffer_load_b16(rsrc, voff, so, 0)));
-                    ny[u] = __half2float(__ushort_as_half(__builtin_amdgcn_raw_buffer_load_b16(rsrc, voff, so + s4, 0)));
-                }
-            }
-        }
-    }
-    // the pixel's records at rank t (the reference's operands only: the vote
-    // kernel makes the fast test's, prep_compacted, while it stages them)
-    __device__ __forceinline__ void gather_store(float4 *eb, int64_t P, int64_t t, int r, int c, bool f) {
-        for (int v0 = 0; v0 < vn; v0 += kCompactKp) {
-            if (v0 > 0) load(v0, f);
-            if (f) {
-#pragma unroll
-                for (int u = 0; u < kCompactKp; ++u) {
-                    if (v0 + u >= vn) break;
-                    eb[(int64_t)(v0 + u) * P + t] = make_float4((float)c, (float)r, nx[u], ny[u]);
-                }
-            }
-        }
-    }
-};
-
-// Sum over j < upto of a look-back array's entries (count + 1), the block's
-// threads striding over j; an entry still 0 after kLookbackSpin is replaced by
-// self(j), the same count worked out by the waiting thread.
-__device__ int g_lb_self;   // debug (pv_debug_lookback_self): every count worked out by the waiter itself
-
-template <typename Self>
-__device__ __forceinline__ int lookback_sum(const int32_t *flag, int upto, int *sh, Self self) {
-    int pre = 0;
-    const bool force = g_lb_self != 0;
-    for (int j = threadIdx.x; j < upto; j += 256) {
-        int v = force ? 0 : ld_agent(&flag[j]);
-        if (v == 0 && !force) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            while ((v = ld_agent(&flag[j])) == 0 && __builtin_amdgcn_s_memrealtime() - t0 < kLookbackSpin)
-                __builtin_amdgcn_s_sleep(1);
-        }
-        pre += v != 0 ? v - 1 : self(j);
-    }
-    return block_sum2(pre, 0, sh).x;
-}
+constexpr uint64_t kLookbackSpin = 20000;   // s_memrealtime ticks (100 MHz): 200 us
+__device__ int g_lb_self;   // debug (pv_debug_lookback_self): every look-back count worked out by the waiter
 
 template <int KIND, bool EVD, int VK>
-__global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int H, int W, int vn, int nblk,
-                                                 int min_num, int max_num, uint64_t *fgbits, int32_t *lbflag,
-                                                 int32_t *tn, int32_t *fgtot, float4 *pex, int32_t *zero,
-                                                 int64_t zero_words) {
+__global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int H, int W, int vn,
+                                                 const int32_t *blkcnt, const uint64_t *fgbits, int32_t *dsagg,
+                                                 int nblk, int min_num, int max_num, uint64_t seed,
+                                                 const uint8_t *keep, int32_t *tn, int32_t *fgtot, float4 *pex) {
     static_assert(kCompactChunk == 256, "one pixel per thread");
     const int b = blockIdx.y, blk = blockIdx.x;
     const int64_t P = (int64_t)H * W;
@@ -380,52 +318,118 @@ __global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int 
     __shared__ int sh[8];
     __shared__ int wcnt[4];
     cstamp(blk, 0);
+    // one round trip: this wave's foreground ballot (k_fg_count) beside the
+    // image's per-block counts (the total and this block's row-major offset)
+    const uint64_t fw = fgbits[((int64_t)b * nblk + blk) * 4 + wid];
+    int2 tot = image_totals(blkcnt + b * nblk, nblk, blk, sh);
+    cstamp(blk, 1);
+    const int fgb = tot.x;
+    if (fgb < min_num) {
+        if (blk == 0 && threadIdx.x == 0) { tn[b] = 0; fgtot[b] = fgb; }
+        return;
+    }
+    const bool ds = fgb > max_num;
+    int base = tot.y;
+    if (!ds && blk == 0 && threadIdx.x == 0) {
+        tn[b] = fgb;
+        fgtot[b] = fgb;
+    }
     const uint32_t p = (uint32_t)blk * kCompactChunk + threadIdx.x;   // H, W <= 65535: fits
-    const int r = (int)(p / (uint32_t)W), c = (int)(p - (uint32_t)r * W);
-    const bool f = p < P && is_fg<KIND, EVD>(m, b, r, c);
-    {   // zero counts + tickets (read only by later kernels of this pipeline)
-        int64_t g = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x;
-        int64_t G = (int64_t)gridDim.x * gridDim.y * 256;
-        for (int64_t i = g; i < zero_words; i += G) zero[i] = 0;
-    }
-    const uint64_t bal = ballot(f);
+    bool f = (fw >> lane) & 1;
+    if (ds && f) f = keep ? keep[b * P + p] != 0 : rand_unit(seed, (uint64_t)b * P + p) < (float)max_num / (float)fgb;
+    const uint64_t bal = ds ? ballot(f) : fw;
     const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-    if (lane == 0) {
-        fgbits[((int64_t)b * nblk + blk) * 4 + wid] = bal;
-        wcnt[wid] = __popcll(bal);
-    }
-    // the pixel's vertex loads, in flight across the look-back
-    VertexGather<VK> vg(vx, b, r, c, vn);
-    vg.load(0, f);
+    if (lane == 0) wcnt[wid] = __popcll(bal);
+    // this pixel's vertex loads (all keypoints of a group in flight together),
+    // issued before the block's offsets are known: buffer loads through a
+    // per-image descriptor, one VGPR offset for the pixel and the keypoint /
+    // component plane offsets in SGPRs (host check: the image's view spans
+    // < 2 GiB)
+    const int r = (int)(p / (uint32_t)W), c = (int)(p - (uint32_t)r * W);
+    constexpr int ES = VK == PV_VERTEX_F32 ? 4 : 2;
+    const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)((const char *)vx.p + (int64_t)b * vx.s[0] * ES), (short)0, vx.extent, 0x00020000);
+    const int voff = (int)((r * vx.s[1] + c * vx.s[2]) * ES);
+    float nx[kCompactKp], ny[kCompactKp];
+    auto load_group = [&](int v0) {
+#pragma unroll
+        for (int u = 0; u < kCompactKp; ++u) {
+            nx[u] = ny[u] = 0.f;
+            if (f && v0 + u < vn) {
+                const int so = uniform((int)((v0 + u) * vx.s[3] * ES));
+                const int s4 = uniform((int)(vx.s[4] * ES));
+                if constexpr (VK == PV_VERTEX_F32) {
+                    nx[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vr, voff, so, 0));
+                    ny[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vr, voff, so + s4, 0));
+                } else {
+                    nx[u] = __half2float(__ushort_as_half(__builtin_amdgcn_raw_buffer_load_b16(vr, voff, so, 0)));
+                    ny[u] = __half2float(__ushort_as_half(__builtin_amdgcn_raw_buffer_load_b16(vr, voff, so + s4, 0)));
+                }
+            }
+        }
+    };
+    load_group(0);
     __syncthreads();
     const int nsel = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
     int off = below;
     for (int q = 0; q < wid; ++q) off += wcnt[q];
-    int32_t *flag = lbflag + (int64_t)b * nblk;
-    if (threadIdx.x == 0) st_agent(&flag[blk], nsel + 1);
-    cstamp(blk, 1);
-    const int base = lookback_sum(flag, blk, sh, [&](int j) {
-        int n = 0;
-        for (int q = 0; q < kCompactChunk; ++q) {
-            const int64_t pp = (int64_t)j * kCompactChunk + q;
-            if (pp < P) n += is_fg<KIND, EVD>(m, b, (int)(pp / W), (int)(pp % W)) ? 1 : 0;
+    if (ds) {
+        // Downsampled offsets by look-back: publish this block's kept count
+        // (+1, so 0 = not yet; k_fg_count zeroed the array), then add up the
+        // earlier blocks' counts, waiting for each.  No dispatch order is
+        // assumed: a count not seen within kLookbackSpin (a block not yet
+        // scheduled) is worked out by the waiting thread itself from the
+        // foreground ballots and the keep decisions, so every wait ends.
+        int32_t *agg = dsagg + (int64_t)b * nblk;
+        if (threadIdx.x == 0) {
+            st_agent(&agg[blk], nsel + 1);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        return n;
-    });
-    cstamp(blk, 2);
-    if (blk == nblk - 1 && threadIdx.x == 0) {
-        const int fg = base + nsel;
-        fgtot[b] = fg;
-        tn[b] = fg < min_num || fg > max_num ? 0 : fg;   // fg > max_num: k_dsample_hyp writes tn
+        const bool self_all = g_lb_self != 0;
+        int pre = 0;
+        for (int j = threadIdx.x; j < blk; j += 256) {
+            int v = self_all ? 0 : ld_agent(&agg[j]);
+            if (v == 0 && !self_all) {
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                while ((v = ld_agent(&agg[j])) == 0 && __builtin_amdgcn_s_memrealtime() - t0 < kLookbackSpin)
+                    __builtin_amdgcn_s_sleep(1);
+            }
+            if (v == 0) {   // block j's kept count from its ballots
+                for (int q = 0; q < 4; ++q) {
+                    uint64_t w = fgbits[((int64_t)b * nblk + j) * 4 + q];
+                    while (w) {
+                        const uint32_t pj = (uint32_t)j * kCompactChunk + q * 64 + __builtin_ctzll(w);
+                        w &= w - 1;
+                        v += keep ? keep[b * P + pj] != 0
+                                  : rand_unit(seed, (uint64_t)b * P + pj) < (float)max_num / (float)fgb;
+                    }
+                }
+                ++v;
+            }
+            pre += v - 1;
+        }
+        base = block_sum2(pre, 0, sh).x;
+        if (blk == nblk - 1 && threadIdx.x == 0) { tn[b] = base + nsel; fgtot[b] = fgb; }
     }
-    vg.gather_store(pex + (int64_t)b * vn * P, P, base + off, r, c, f);
+    cstamp(blk, 2);
+    // the selected pixel's records at t = base + its rank: consecutive
+    // selected pixels write consecutive records of each keypoint
+    float4 *eb = pex + (int64_t)b * vn * P;
+    const int64_t t = base + off;
+    for (int v0 = 0; v0 < vn; v0 += kCompactKp) {
+        if (v0 > 0) load_group(v0);
+        if (f) {
+#pragma unroll
+            for (int u = 0; u < kCompactKp; ++u) {
+                if (v0 + u >= vn) break;
+                const int64_t o = (int64_t)(v0 + u) * P + t;
+                // the reference's operands only: the vote kernel makes the fast
+                // test's (prep_compacted) while it stages them
+                eb[o] = make_float4((float)c, (float)r, nx[u], ny[u]);
+            }
+        }
+    }
     cstamp(blk, 3);
-}
-
-// downsampling keep decision of foreground pixel p (RV:543-546)
-__device__ __forceinline__ bool ds_keep(const uint8_t *keep, uint64_t seed, int b, int64_t P, uint32_t p, int max_num,
-                                        int fg) {
-    return keep ? keep[b * P + p] != 0 : rand_unit(seed, (uint64_t)b * P + p) < (float)max_num / (float)fg;
 }
 
 // ==========================================================================
@@ -475,7 +479,7 @@ struct VoteArgs {
     const float2 *raw;          // !PREPPED: raw[b*vn*P + v*raw_v + t*raw_t]
     const float2 *hyp;          // !GEN: hyp[b*hyp_sb + v*hyp_sv + h*hyp_sh]
     float2 *hyp_out;            // GEN: generated hypotheses [b][nh][vn]
-    float2 *hypv_out;           // k_dsample_hyp: keypoint-major copy [b][vn][nh]
+    float2 *hypv_out;           // k_hyp_gen: keypoint-major copy [b][vn][nh]
     int64_t hyp_sb, hyp_sv, hyp_sh;
     float *diag_hyp;            // GEN: optional copy [b][nh][vn][2]
     const int32_t *idxs;        // GEN: pixel pairs [b][nh][vn][2], or nullptr (counter RNG)
@@ -1144,135 +1148,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     }
 }
 
-// ==========================================================================
-// K2: the downsampling pass (RV:543-546) and the hypotheses (KU:11-49), one
-// launch.
-// Blocks [0, b * nsb): downsampling super-blocks of kDsChunks compaction
-// blocks.  For an image with fg <= max_num (the usual case) a super-block
-// only returns k_compact's look-back flags to zero.  Otherwise its kept
-// pixels (Bernoulli(max_num / fg) by the counter RNG, or the caller's keep
-// mask) are compacted again from the vertex field in row-major order, ranked
-// by a look-back over the super-blocks (the same self-counting fallback as
-// k_compact), and the image's last super-block to finish (a ticket) makes the
-// image's hypotheses.
-// Blocks [b * nsb, ...): one thread per (image, hypothesis, keypoint) of the
-// images not downsampled: the pixel pair (the caller's idxs or the counter
-// RNG, RV:553) and its intersection, stored in the reference layout and
-// keypoint-major (a.hypv_out; no such blocks when the vote kernel makes its
-// own).  Images without a vote are left alone.
-// ==========================================================================
-constexpr int kDsChunks = 4;
-
-struct DsArgs {
-    VertexView vx;
-    int H, W, vn, nblk, nsb, nb, min_num, max_num;
-    uint64_t seed;
-    const uint8_t *keep;
-    const uint64_t *fgbits;
-    int32_t *dsagg, *dsdone, *lbflag, *tn;
-    const int32_t *fgtot;
-    float4 *pex;
-};
-
-template <int VK>
-__global__ __launch_bounds__(256) void k_dsample_hyp(DsArgs d, VoteArgs a) {
-    const int nds = d.nb * d.nsb;
-    if ((int)blockIdx.x < nds) {
-        const int b = blockIdx.x / d.nsb, sb = blockIdx.x - b * d.nsb;
-        const int wid = threadIdx.x / 64, lane = lane_id();
-        const int c0 = sb * kDsChunks;
-        if (threadIdx.x < kDsChunks && c0 + (int)threadIdx.x < d.nblk)
-            d.lbflag[(int64_t)b * d.nblk + c0 + threadIdx.x] = 0;
-        const int fg = d.fgtot[b];
-        if (fg < d.min_num || fg <= d.max_num) return;
-        const int64_t P = (int64_t)d.H * d.W;
-        const uint64_t *fb = d.fgbits + (int64_t)b * d.nblk * 4;
-        __shared__ int sh[8];
-        __shared__ int wc[kDsChunks][4];
-        __shared__ int slast;
-        bool f[kDsChunks];
-        int off[kDsChunks];
-#pragma unroll
-        for (int k = 0; k < kDsChunks; ++k) {
-            const int cc = c0 + k;
-            const uint32_t p = (uint32_t)cc * kCompactChunk + threadIdx.x;
-            const uint64_t fw = cc < d.nblk ? fb[cc * 4 + wid] : 0;
-            bool fk = (fw >> lane) & 1;
-            if (fk) fk = ds_keep(d.keep, d.seed, b, P, p, d.max_num, fg);
-            const uint64_t bal = ballot(fk);
-            off[k] = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-            if (lane == 0) wc[k][wid] = __popcll(bal);
-            f[k] = fk;
-        }
-        __syncthreads();
-        int nsel = 0;
-#pragma unroll
-        for (int k = 0; k < kDsChunks; ++k) {
-            off[k] += nsel;
-            for (int q = 0; q < wid; ++q) off[k] += wc[k][q];
-            nsel += wc[k][0] + wc[k][1] + wc[k][2] + wc[k][3];
-        }
-        int32_t *agg = d.dsagg + (int64_t)b * d.nblk;
-        if (threadIdx.x == 0) st_agent(&agg[sb], nsel + 1);
-        const int base = lookback_sum(agg, sb, sh, [&](int j) {
-            int n = 0;
-            for (int k = 0; k < kDsChunks; ++k) {
-                const int cc = j * kDsChunks + k;
-                if (cc >= d.nblk) break;
-                for (int q = 0; q < 4; ++q) {
-                    uint64_t w = fb[cc * 4 + q];
-                    while (w) {
-                        const int bit = __builtin_ctzll(w);
-                        w &= w - 1;
-                        n += ds_keep(d.keep, d.seed, b, P, (uint32_t)cc * kCompactChunk + q * 64 + bit, d.max_num, fg);
-                    }
-                }
-            }
-            return n;
-        });
-        if (sb == d.nsb - 1 && threadIdx.x == 0) d.tn[b] = base + nsel;
-        float4 *eb = d.pex + (int64_t)b * d.vn * P;
-        for (int k = 0; k < kDsChunks; ++k) {
-            const uint32_t p = (uint32_t)(c0 + k) * kCompactChunk + threadIdx.x;
-            const int r = (int)(p / (uint32_t)d.W), c = (int)(p - (uint32_t)r * d.W);
-            VertexGather<VK> vg(d.vx, b, r, c, d.vn);
-            vg.load(0, f[k]);
-            vg.gather_store(eb, P, base + off[k], r, c, f[k]);
-        }
-        // hand-off to the image's last super-block (MI355X_MICROARCH.md
-        // "Valid forms": plain stores, every wave's wait, barrier, agent
-        // release, relaxed ticket; the consumer's one agent acquire)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            slast = __hip_atomic_fetch_add(&d.dsdone[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == d.nsb - 1;
-        }
-        __syncthreads();
-        if (!slast || !a.hypv_out) return;
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-        const int n = d.tn[b];
-        if (n <= 0) return;
-        for (int i = threadIdx.x; i < a.nh * a.vn; i += 256) {
-            const int h = i / a.vn, v = i - h * a.vn;
-            a.hypv_out[((int64_t)b * a.vn + v) * a.nh + h] = item_hyp<true, true>(a, b, v, h, true, n, true);
-        }
-        return;
-    }
+// Hypotheses once per launch (pipeline, hyp_pregen), one thread per
+// (image, hypothesis, keypoint): the pixel pair (the caller's idxs or the
+// counter RNG, RV:553) and its intersection (KU:11-49), stored in the
+// reference layout and keypoint-major; images without a vote are left alone.
+__global__ __launch_bounds__(256) void k_hyp_gen(VoteArgs a) {
     const int64_t per = (int64_t)a.nh * a.vn;
-    const int64_t gid = (int64_t)(blockIdx.x - nds) * 256 + threadIdx.x;
+    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (gid >= per * a.b) return;
     const int b = (int)(gid / per);
     const int r = (int)(gid - b * per);
     const int h = r / a.vn, v = r - h * a.vn;
-    const int fg = d.fgtot[b];
-    if (fg >= d.min_num && fg > d.max_num) return;     // downsampled: its last super-block makes them
-    const int n = a.tn_dev[b];
+    const int n = a.tn_dev ? a.tn_dev[b] : a.tn_host;
     if (n > 0) a.hypv_out[((int64_t)b * a.vn + v) * a.nh + h] = item_hyp<true, true>(a, b, v, h, true, n, true);
 }
 
@@ -1392,7 +1279,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
         for (int i = 0; i < 2; ++i) {
             const int h = hg * kGroup + i * kWave + lane;
             const bool hl = h < a.nh;
-            // pre-generated (k_dsample_hyp, a.hyp keypoint-major) or made here
+            // pre-generated (k_hyp_gen, a.hyp keypoint-major) or made here
             const float2 hv = a.hyp ? item_hyp<false, PREPPED>(a, b, v, h, hl, n, false)
                                     : item_hyp<PREPPED, PREPPED>(a, b, v, h, hl, n, PREPPED && ts == 0);
             hlds[i * kWave + lane] = hv;
@@ -3015,7 +2902,7 @@ bool vote_old() {
     return g_vote_kernel >= 0 ? g_vote_kernel == 1 : old;
 }
 
-// hypotheses by k_dsample_hyp before the vote (default; PVVOTE_HYPGEN=0 makes
+// hypotheses by k_hyp_gen before the vote (default; PVVOTE_HYPGEN=0 makes
 // them in the vote kernel's prologue instead, read once per process):
 // measured 34.6k -> 36.6k images/s, vote kernel 35.2 -> 31.8 us (every
 // block of a keypoint otherwise gathers and intersects the same 512 pairs)
@@ -3115,15 +3002,16 @@ template <int KIND, bool EVD>
 struct CompactStage {
     static int run(const CompactArgs *a) {
         dim3 grid(a->nblk, a->b);
-        const Workspace &w = a->ws;
+        k_fg_count<KIND, EVD><<<grid, 256, 0, a->s>>>(a->m, a->H, a->W, a->ws.blkcnt, a->ws.fgbits, a->nblk, a->ws.counts,
+                                                      a->ws.zero_words);
         if (a->vx.kind == PV_VERTEX_F32)
-            k_compact<KIND, EVD, PV_VERTEX_F32><<<grid, 256, 0, a->s>>>(a->m, a->vx, a->H, a->W, a->vn, a->nblk,
-                                                                         a->min_num, a->max_num, w.fgbits, w.lbflag,
-                                                                         w.tn, w.fgtot, w.pex, w.counts, w.zero_words);
+            k_compact<KIND, EVD, PV_VERTEX_F32><<<grid, 256, 0, a->s>>>(a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.fgbits, a->ws.dsagg,
+                                                     a->nblk, a->min_num, a->max_num, a->seed, a->keep, a->ws.tn,
+                                                     a->ws.fgtot, a->ws.pex);
         else
-            k_compact<KIND, EVD, PV_VERTEX_F16><<<grid, 256, 0, a->s>>>(a->m, a->vx, a->H, a->W, a->vn, a->nblk,
-                                                                         a->min_num, a->max_num, w.fgbits, w.lbflag,
-                                                                         w.tn, w.fgtot, w.pex, w.counts, w.zero_words);
+            k_compact<KIND, EVD, PV_VERTEX_F16><<<grid, 256, 0, a->s>>>(a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.fgbits, a->ws.dsagg,
+                                                     a->nblk, a->min_num, a->max_num, a->seed, a->keep, a->ws.tn,
+                                                     a->ws.fgtot, a->ws.pex);
         return last();
     }
 };
@@ -3182,26 +3070,16 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
     va.b = b; va.vn = vn; va.nh = nh; va.hgn = (nh + kGroup - 1) / kGroup;
     fast_constants(prm->inlier_thresh, &va);
     va.trace = g_vote_trace;
-    // the downsampling pass (a no-op but for the look-back flags unless an
-    // image has fg > max_num) and, by default (hyp_pregen), the hypotheses,
-    // which the vote kernel (k_vote_mfma) then reads keypoint-major; else the
-    // vote kernel makes them in its prologue and stores the reference layout
-    const bool pregen = hyp_pregen() && va.hgn % 4 == 0 && !vote_old();
-    {
-        DsArgs d{};
-        d.vx = ca.vx; d.H = H; d.W = W; d.vn = vn; d.nblk = nblk;
-        d.nsb = (nblk + kDsChunks - 1) / kDsChunks; d.nb = b;
-        d.min_num = ca.min_num; d.max_num = ca.max_num; d.seed = ca.seed; d.keep = ca.keep;
-        d.fgbits = w.fgbits; d.dsagg = w.dsagg; d.dsdone = w.dsdone; d.lbflag = w.lbflag; d.tn = w.tn;
-        d.fgtot = w.fgtot; d.pex = w.pex;
-        if (pregen) va.hypv_out = w.hypv;
-        const int64_t nt = pregen ? (int64_t)b * nh * vn : 0;
-        const int64_t grid = (int64_t)b * d.nsb + (nt + 255) / 256;
-        if (grid >= (1ll << 31)) return PV_EINVAL;
-        if (img->vertex_kind == PV_VERTEX_F32) k_dsample_hyp<PV_VERTEX_F32><<<(unsigned)grid, 256, 0, s>>>(d, va);
-        else k_dsample_hyp<PV_VERTEX_F16><<<(unsigned)grid, 256, 0, s>>>(d, va);
+    // the vote kernel generates the hypotheses itself (item_hyp in its
+    // prologue, overlapped with its first pixel loads) and stores them in
+    // the reference layout; by default (hyp_pregen) one k_hyp_gen launch makes
+    // them first and the vote kernel (k_vote_mfma) reads them keypoint-major
+    if (hyp_pregen() && va.hgn % 4 == 0 && !vote_old()) {
+        va.hypv_out = w.hypv;
+        const int64_t nt = (int64_t)b * nh * vn;
+        k_hyp_gen<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(va);
         if ((r = last())) return r;
-        if (pregen) { va.hyp = w.hypv; va.hyp_sb = (int64_t)vn * nh; va.hyp_sv = nh; va.hyp_sh = 1; }
+        va.hyp = w.hypv; va.hyp_sb = (int64_t)vn * nh; va.hyp_sv = nh; va.hyp_sh = 1;
     }
     if (dg.ev_vote_begin) {
         hipError_t e = hipEventRecord((hipEvent_t)dg.ev_vote_begin, s);
@@ -3371,8 +3249,8 @@ int pv_debug_wave_minmax(const float *in, float *out, int32_t nwaves, pv_stream_
     return last();
 }
 
-// debug only (not in pvvote.h): the compaction look-backs count every earlier
-// block themselves instead of reading its flag (tests of the fallback path)
+// debug only (not in pvvote.h): the downsampling look-back counts every earlier
+// block itself instead of reading its count (tests of the fallback path)
 int pv_debug_lookback_self(int32_t on) {
     return rc(hipMemcpyToSymbol(HIP_SYMBOL(g_lb_self), &on, sizeof(on)));
 }
@@ -3402,10 +3280,7 @@ int pv_debug_compact_trace(int on, uint64_t *host, int n) {
 
 size_t pv_v3_workspace_size(int32_t b, int32_t H, int32_t W, int32_t vn, int32_t n_hyp) {
     if (b <= 0 || H <= 0 || W <= 0 || vn <= 0 || n_hyp <= 0) return 0;
-    const Workspace r = carve(nullptr, 0, b, H, W, vn, n_hyp);   // the rest, from offset 0
-    // T / 256 - 256 >= the flags and T * 255 / 256 >= the rest: ws_fits(carve(T), T)
-    const size_t t = std::max<size_t>(256 * ((size_t)r.flag_bytes + 256), r.total / 255 * 256 + 65536);
-    return (size_t)align_up((int64_t)t, 256);
+    return carve(nullptr, b, H, W, vn, n_hyp).total;
 }
 
 int pv_ransac_voting_v3(const pv_image_desc *img, const pv_vote_params *prm, float *out, void *workspace,
@@ -3414,8 +3289,8 @@ int pv_ransac_voting_v3(const pv_image_desc *img, const pv_vote_params *prm, flo
     if (r) return r;
     if (!prm || !out || prm->round_hyp_num <= 0) return PV_EINVAL;
     const int nh = prm->round_hyp_num;
-    Workspace w = carve(workspace, workspace_bytes, img->b, img->H, img->W, img->vn, nh);
-    if (!ws_fits(w, workspace, workspace_bytes)) return PV_EWORKSPACE;
+    Workspace w = carve(workspace, img->b, img->H, img->W, img->vn, nh);
+    if (!workspace || workspace_bytes < w.total) return PV_EWORKSPACE;
     hipStream_t s = (hipStream_t)stream;
     pv_v3_diag dg{};
     if (diag) dg = *diag;
@@ -3441,7 +3316,7 @@ int pv_ransac_voting_v5(const pv_image_desc *img, const pv_vote_params *prm, flo
     if (!conf) return PV_EINVAL;
     int r = pv_ransac_voting_v3(img, prm, out, workspace, workspace_bytes, diag, stream);
     if (r) return r;
-    Workspace w = carve(workspace, workspace_bytes, img->b, img->H, img->W, img->vn, prm->round_hyp_num);
+    Workspace w = carve(workspace, img->b, img->H, img->W, img->vn, prm->round_hyp_num);
     const int64_t P = (int64_t)img->H * img->W;
     k_point_conf<<<dim3(kRefineNJ, img->vn, img->b), 256, 0, (hipStream_t)stream>>>(out, w.pex, w.tn, P, img->vn,
                                                                                      conf_thresh, w.confc, conf);
@@ -3482,8 +3357,8 @@ static int evd_front(const pv_image_desc *img, const pv_vote_params *prm, void *
     if (!prm || prm->round_hyp_num <= 0 || prm->min_hyp_num <= 0) return PV_EINVAL;
     int rounds = (prm->min_hyp_num + prm->round_hyp_num - 1) / prm->round_hyp_num;
     *nh = rounds * prm->round_hyp_num;
-    *w = carve(workspace, workspace_bytes, img->b, img->H, img->W, img->vn, *nh);
-    if (!ws_fits(*w, workspace, workspace_bytes)) return PV_EWORKSPACE;
+    *w = carve(workspace, img->b, img->H, img->W, img->vn, *nh);
+    if (!workspace || workspace_bytes < w->total) return PV_EWORKSPACE;
     pv_v3_diag none{};
     return front_half(img, prm, *nh, true, *w, none, s);
 }

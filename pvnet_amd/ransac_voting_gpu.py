@@ -81,10 +81,7 @@ class VotingWorkspace:
             if buf is not None:
                 for st in self._streams.get(key, ()):
                     buf.record_stream(st)
-            # zero-filled once: the pipelines' look-back flags start zero and
-            # every call leaves them zero (pvvote.h, pv_v3_workspace_size);
-            # each call passes the buffer's full byte count
-            buf = torch.zeros(max(nbytes, 1), dtype=torch.uint8, device=device)
+            buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
             self._buf[key] = buf
             self._streams[key] = set()
         self._streams[key].add(stream)
@@ -185,13 +182,13 @@ def _v3(d, mask, vertex, round_hyp_num, inlier_thresh, confidence, max_iter, min
     conf = None
     with torch.cuda.device(dev):
         if conf_thresh is None:
-            code = L.pv_ransac_voting_v3(ctypes.byref(d), ctypes.byref(prm), out.data_ptr(), ws.data_ptr(), ws.numel(),
+            code = L.pv_ransac_voting_v3(ctypes.byref(d), ctypes.byref(prm), out.data_ptr(), ws.data_ptr(), nbytes,
                                          ctypes.byref(diag) if diag is not None else None,
                                          torch.cuda.current_stream(dev).cuda_stream)
         else:
             conf = torch.empty((b, vn), dtype=torch.float32, device=dev)
             code = L.pv_ransac_voting_v5(ctypes.byref(d), ctypes.byref(prm), float(conf_thresh), out.data_ptr(),
-                                         conf.data_ptr(), ws.data_ptr(), ws.numel(),
+                                         conf.data_ptr(), ws.data_ptr(), nbytes,
                                          ctypes.byref(diag) if diag is not None else None,
                                          torch.cuda.current_stream(dev).cuda_stream)
     _lib.check(code, "ransac_voting_layer_v3" if conf_thresh is None else "ransac_voting_layer_v5")
@@ -267,7 +264,7 @@ def _evd_common(mask, vertex, round_hyp_num, min_hyp_num, inlier_thresh, min_num
     L = _lib.load()
     nbytes = L.pv_v3_workspace_size(d.b, d.H, d.W, d.vn, nh)
     ws = (_workspace or _default_ws).get(dev, nbytes)
-    return d, prm, ws, ws.numel(), (idxs, keep)
+    return d, prm, ws, nbytes, (idxs, keep)
 
 
 def estimate_voting_distribution_with_mean(mask, vertex, mean, round_hyp_num=256, min_hyp_num=4096, topk=128,

@@ -612,34 +612,28 @@ def test_both_vote_kernels_bit_exact(kernel, device, rvg):
 
 
 def test_compaction_lookback_self_count_fallback(device, rvg):
-    """The single-pass compaction's look-back (k_compact) and the downsampling
-    pass's (k_dsample_hyp) with every earlier block's count worked out by the
-    waiting thread itself -- the path a block takes when a predecessor has not
-    been scheduled within the spin limit -- give the golden results (plain and
-    downsampled cat, the edge cases)."""
+    """The downsampling look-back of k_compact with every earlier block's kept
+    count worked out by the waiting thread itself -- the path a block takes
+    when a predecessor has not been scheduled within the spin limit -- gives
+    the golden results (downsampled cat, the downsampled edge case)."""
     L = _lib.load()
     L.pv_debug_lookback_self.argtypes = [ctypes.c_int32]
     L.pv_debug_lookback_self.restype = ctypes.c_int32
     assert L.pv_debug_lookback_self(1) == 0
     try:
-        g = G.load("cat_v3_512")
-        mask, vertex, _ = G.cat_inputs(g)
-        run_v3(rvg, mask, vertex, g, "", device)
         g = G.load("cat_v3_128_maxnum100")
         mask, vertex, _ = G.cat_inputs(g)
         keep = np.unpackbits(g["keep_bits"][0])[: 480 * 640].reshape(1, 480, 640)
         run_v3(rvg, mask, vertex, g, "", device, keep=keep, max_num=100)
         g = G.load("edge_cases")
-        run_v3(rvg, g["a_mask"], g["a_vertex"], g, "a_", device)
         run_v3(rvg, g["d_mask"], g["d_vertex"], g, "d_", device, keep=g["d_keep"].astype(np.uint8), max_num=300)
     finally:
         L.pv_debug_lookback_self(0)
 
 
 def test_workspace_reused_across_shapes(device, rvg):
-    """One workspace through calls of different shapes, downsampled and not
-    (the look-back flags' region depends only on the buffer's size and every
-    call leaves it zero): each call matches its golden results."""
+    """One workspace through calls of different shapes, downsampled and not:
+    each call matches its golden results (no state carried between calls)."""
     ws = rvg.VotingWorkspace()
     gs = G.load("synth_v3_512")
     ms, vs, _ = G.synth_inputs(gs)

@@ -38,6 +38,6 @@ for name in sorted({e[2] for e in ev}):
     out[name] = rec
 if len(sys.argv) > 2:
     json.dump(out, open(sys.argv[2], "w"), indent=1)
-for k in ("k_compact", "k_dsample_hyp", "k_vote_mfma", "k_vote_count", "k_refine_solve", "k_vote_bytes"):
+for k in ("k_fg_count", "k_compact", "k_hyp_gen", "k_vote_mfma", "k_vote_count", "k_refine_solve", "k_vote_bytes"):
     if k in out:
         print(k, out[k])

@@ -12,7 +12,7 @@ timeout -k 10 500 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$P
 grep '^{' gpurun_out/bench_prof.log | tail -1 > gpurun_out/bench_prof.json
 if [ -n "$PMC" ]; then
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 400 rocprofv3 --kernel-include-regex "k_vote|k_compact|k_dsample|k_refine" --pmc $c -T --output-format csv \
+    timeout -k 10 400 rocprofv3 --kernel-include-regex "k_vote|k_compact|k_fg_count|k_refine|k_hyp_gen|k_front" --pmc $c -T --output-format csv \
       -d "$PWD/gpurun_out/pmc_$c" -o b -- python3 bench.py --steps 5 --warmup 2 --skip-cpu --skip-e2e > gpurun_out/pmc_$c.log 2>&1 || { echo "pmc $c failed"; exit 1; }
   done
   python3 tools/pmc_traffic_json.py gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE gpurun_out/pmc_traffic.json > /dev/null
