@@ -635,10 +635,10 @@ constexpr int kGroup = kWave * kHypLane;
 // The wave's slab of exact operands.  Pipeline pixels are integer centres
 // below 65536 (check_desc), packed as cx | cy << 16: 12 B per pixel keeps a
 // block at 28 KiB of LDS (5 blocks per CU); API coordinates are any floats.
-template <bool PACKED>
+template <bool PACKED, int N = kVoteChunk>
 struct ExactSlab {
-    float2 n[kVoteChunk];
-    uint32_t c[kVoteChunk];
+    float2 n[N];
+    uint32_t c[N];
     __device__ __forceinline__ void put(int j, const F4 &e) {
         n[j] = make_float2(e.z, e.w);
         c[j] = (uint32_t)e.x | ((uint32_t)e.y << 16);
@@ -649,9 +649,9 @@ struct ExactSlab {
         return F4{(float)(q & 0xffffu), (float)(q >> 16), d.x, d.y};
     }
 };
-template <>
-struct ExactSlab<false> {
-    F4 e[kVoteChunk];
+template <int N>
+struct ExactSlab<false, N> {
+    F4 e[N];
     __device__ __forceinline__ void put(int j, const F4 &x) { e[j] = x; }
     __device__ __forceinline__ F4 get(int j) const { return e[j]; }
 };
@@ -1196,7 +1196,10 @@ typedef _Float16 h4f __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kMB = 16;                        // pixels per MFMA batch (32 rows: 16 pixels x (X, Y))
-constexpr int kMBatch = kVoteChunk / kMB;      // batches per sub-chunk (16)
+constexpr int kMChunk = 384;                   // pixels per sub-chunk: a unit's range (~350 px at configs[1]) in one
+constexpr int kMSlots = (kMChunk + 255) / 256; // pixels per thread in the block's staging (2)
+constexpr int kMBatch = kMChunk / kMB;         // batches per sub-chunk (24)
+static_assert(kMChunk % kMB == 0 && kMBatch <= 32 && kMChunk <= 512, "hit masks: 2 x 64 bits; queue: 9-bit pixel");
 constexpr int kMSet = 4;                       // 32-hypothesis column sets per wave (128 hypotheses)
 constexpr float kMHypMax = 8.0e6f;             // |hx|, |hy| above -> exact-only (keeps s >= 2^-9)
 constexpr float kMRMax = 30000.f;              // sub-chunk radius above -> exact sub-chunk (fp16 range of b)
@@ -1204,8 +1207,8 @@ constexpr int kMQueue = 256;                   // band pairs queued per wave bef
 
 template <bool PREPPED>
 struct MSlab {
-    uint4 rows[kMBatch][2 * kMB];              // [batch][row = 2 pixel + form (X, Y)]: k 0..7 as 8 halves (8 KiB)
-    ExactSlab<PREPPED> x;
+    uint4 rows[kMBatch][2 * kMB];              // [batch][row = 2 pixel + form (X, Y)]: k 0..7 as 8 halves (12 KiB)
+    ExactSlab<PREPPED, kMChunk> x;
 };
 
 __device__ __forceinline__ uint32_t pack_h2(_Float16 lo, _Float16 hi) {
@@ -1249,6 +1252,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
     else even_share(total, nunits, (uint32_t)unit, &lo, &hi);
     int buf = 0, nfix = 0, nseg = 0, nslow = 0, nxo = 0;
     uint64_t tloop = 0, t_total = 0, t_hyp = 0;
+    uint64_t c_stage = 0, c_hot = 0, c_fix = 0, c_seg = 0, c_mark = 0;   // debug: shader cycles per phase
+    auto cyc = [&]() -> uint64_t { return a.trace ? __builtin_amdgcn_s_memtime() : 0; };
     if (a.trace) t_total = __builtin_amdgcn_s_memrealtime();
     const float tau = a.tau;
     constexpr float kBig = 3.0e38f;
@@ -1265,13 +1270,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
         const int v = uniform(g / ggn), gg = g - (g / ggn) * ggn;
         const int hg = uniform(gg * 4 + wid);
         // ---- segment: pixels [ts, te) of (b, v) against hypotheses hg*128 .. +127 ----
+        c_mark = cyc();
+        F4 L[kMSlots];
         auto load_px = [&](int s0, int np) {
-            const int t = wid * kWave + lane;
-            F4 e{0.f, 0.f, 0.f, 0.f};
-            if (t < np) e = pixel_exact<PREPPED>(a, b, v, s0 + t);
-            return e;
+#pragma unroll
+            for (int k = 0; k < kMSlots; ++k) {
+                const int t = k * 256 + wid * kWave + lane;
+                L[k] = F4{0.f, 0.f, 0.f, 0.f};
+                if (t < np) L[k] = pixel_exact<PREPPED>(a, b, v, s0 + t);
+            }
         };
-        F4 L = load_px(ts, min(kVoteChunk, te - ts));
+        load_px(ts, min(kMChunk, te - ts));
         // hypotheses: lane makes h = hg*128 + i*64 + lane (i = 0, 1), stored at
         // [set 2i + half][col] -- the same linear index
         uint32_t hfm = 0, hxm = 0;              // per set: fast / exact-only (bit j)
@@ -1301,34 +1310,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
         corr[lane] = 0;
         corr[64 + lane] = 0;
         if (a.trace && t_hyp == 0) t_hyp = __builtin_amdgcn_s_memrealtime();
-        for (int s0 = ts; s0 < te; s0 += kVoteChunk) {
-            const int np = uniform(min(kVoteChunk, te - s0));
+        for (int s0 = ts; s0 < te; s0 += kMChunk) {
+            {
+                const uint64_t t = cyc();
+                if (s0 == ts) c_seg += t - c_mark; else c_fix += t - c_mark;
+                c_mark = t;
+            }
+            const int np = uniform(min(kMChunk, te - s0));
             MSlab<PREPPED> &S = slab[buf];
             QuarterBoxes &QB = qb_all[buf];
             buf ^= 1;
-            // ---- stage: one pixel per thread; the origin is the centre of the
-            // sub-chunk's bounding box (block reduce), so |c'| <= R is small ----
+            // ---- stage: pixels t and 256 + t of thread t; the origin is the
+            // centre of the sub-chunk's bounding box (block reduce), so |c'| <= R
+            // is small ----
             const int t = wid * kWave + lane;
             bool exo_p = false;
-            float xl = kBig, xh = -kBig, yq = 0.f;
-            float4 q = make_float4(__builtin_nanf(""), 0.f, 0.f, 0.f);
-            if (t < np) {
-                const F4 e = L;
-                if (PREPPED) q = prep_compacted(e, &exo_p);
-                else { q = prep_pixel(e.x, e.y, e.z, e.w); exo_p = pixel_exotic(e.z, e.w); }
-                S.x.put(t, e);
-                xl = e.x; xh = e.x; yq = q.y;
+            float xl = kBig, xh = -kBig;
+            float4 q[kMSlots];
+            float yq[kMSlots];
+#pragma unroll
+            for (int k = 0; k < kMSlots; ++k) {
+                const int tt = k * 256 + t;
+                q[k] = make_float4(__builtin_nanf(""), 0.f, 0.f, 0.f);
+                yq[k] = 0.f;
+                if (tt < np) {
+                    const F4 e = L[k];
+                    bool ex = false;
+                    if (PREPPED) q[k] = prep_compacted(e, &ex);
+                    else { q[k] = prep_pixel(e.x, e.y, e.z, e.w); ex = pixel_exotic(e.z, e.w); }
+                    exo_p |= ex;
+                    S.x.put(tt, e);
+                    xl = fminf(xl, e.x); xh = fmaxf(xh, e.x); yq[k] = q[k].y;
+                }
             }
             if (wid * kWave < np) {
                 const float mn = wave_min(xl), mx = wave_max(xh);
                 float yn, yx;
                 if (PREPPED) {
-                    yn = bcast(yq, 0);
-                    yx = bcast(yq, min(kWave - 1, np - 1 - wid * kWave));
+                    // rows never decrease along the compacted order: the wave's
+                    // first pixel (64 wid) and its last (slot 1 when it has one)
+                    yn = bcast(yq[0], 0);
+                    const bool s1 = kMSlots > 1 && 256 + wid * kWave < np;
+                    yx = s1 ? bcast(yq[kMSlots - 1], min(kWave - 1, np - 1 - 256 - wid * kWave))
+                            : bcast(yq[0], min(kWave - 1, np - 1 - wid * kWave));
                 } else {
-                    const bool in = t < np;
-                    yn = wave_min(in ? yq : kBig);
-                    yx = wave_max(in ? yq : -kBig);
+                    float mnq = kBig, mxq = -kBig;
+#pragma unroll
+                    for (int k = 0; k < kMSlots; ++k)
+                        if (k * 256 + t < np) { mnq = fminf(mnq, yq[k]); mxq = fmaxf(mxq, yq[k]); }
+                    yn = wave_min(mnq);
+                    yx = wave_max(mxq);
                 }
                 const uint32_t ex = __builtin_amdgcn_ballot_w64(exo_p) != 0;
                 if (lane == 0) { QB.box[wid] = make_float4(mn, mx, yn, yx); QB.exo[wid] = ex; }
@@ -1337,7 +1368,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                 QB.exo[wid] = 0;
             }
             // next sub-chunk's loads, in flight across the barriers and the hot loop
-            if (s0 + kVoteChunk < te) L = load_px(s0 + kVoteChunk, min(kVoteChunk, te - s0 - kVoteChunk));
+            if (s0 + kMChunk < te) load_px(s0 + kMChunk, min(kMChunk, te - s0 - kMChunk));
             __syncthreads();
             float cxl = kBig, cxh = -kBig, cyl = kBig, cyh = -kBig;
             uint32_t exq = 0;
@@ -1355,18 +1386,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
             bool slow = !a.fast || exq != 0 || !(R <= kMRMax);
             slow = __builtin_amdgcn_readfirstlane(slow);
             nslow += slow ? 1 : 0;
-            {
+#pragma unroll
+            for (int k = 0; k < kMSlots; ++k) {
+                const int tt = k * 256 + t;
+                if (tt >= kMChunk) break;
                 uint4 rx = make_uint4(0u, 0u, pack_h2((_Float16)0.f, (_Float16)0.f),
                                       pack_h2((_Float16)(-60000.f), (_Float16)0.f));   // never votes: X = -6e4 s
                 uint4 ry = make_uint4(0u, 0u, 0u, 0u);
-                if (q.x == q.x && !slow) {
-                    const float cx = q.x - ox, cy = q.y - oy;      // exact for pixel centres
-                    const float axX = tau * q.z, ayX = tau * q.w;
+                if (q[k].x == q[k].x && !slow) {
+                    const float cx = q[k].x - ox, cy = q[k].y - oy;      // exact for pixel centres
+                    const float axX = tau * q[k].z, ayX = tau * q[k].w;
                     rx = form_row(axX, ayX, fmaf(axX, cx, ayX * cy));
-                    ry = form_row(-q.w, q.z, fmaf(-q.w, cx, q.z * cy));
+                    ry = form_row(-q[k].w, q[k].z, fmaf(-q[k].w, cx, q[k].z * cy));
                 }
-                S.rows[t >> 4][2 * (t & 15)] = rx;
-                S.rows[t >> 4][2 * (t & 15) + 1] = ry;
+                S.rows[tt >> 4][2 * (tt & 15)] = rx;
+                S.rows[tt >> 4][2 * (tt & 15) + 1] = ry;
             }
             __syncthreads();
             if (!slow) {
@@ -1395,7 +1429,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                     gb[j] = fj ? (a.gzf + a.gzr) * Bv * s * 1.00001f : -1.f;
                 }
                 uint32_t neg[kMSet] = {0u, 0u, 0u, 0u};
-                uint64_t hitmask = 0;
+                uint64_t hm0 = 0, hm1 = 0;              // band hits: bit 4 p + set, batches 0-15 / 16-31
 #ifdef PVM_ABL_HOT
                 const int nb = 0;
 #else
@@ -1433,6 +1467,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                 // batch are taken together at its end
                 const f32x16 zero = {};
                 if (a.trace && tloop == 0) tloop = __builtin_amdgcn_s_memrealtime();
+                { const uint64_t t = cyc(); c_stage += t - c_mark; c_mark = t; }
                 h4f A = afrag(0);
                 f32x16 c0 = __builtin_amdgcn_mfma_f32_32x32x8f16(A, bf[0], zero, 0, 0, 0);
 #pragma unroll 1
@@ -1450,20 +1485,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                                         (__builtin_amdgcn_ballot_w64(m1 <= gb[1]) != 0 ? 2u : 0u) |
                                         (__builtin_amdgcn_ballot_w64(m2 <= gb[2]) != 0 ? 4u : 0u) |
                                         (__builtin_amdgcn_ballot_w64(m3 <= gb[3]) != 0 ? 8u : 0u);
-                    hitmask |= (uint64_t)hb << (p * kMSet);
+                    const uint64_t hbs = (uint64_t)hb << ((p & 15) * kMSet);
+                    if (p < 16) hm0 |= hbs; else hm1 |= hbs;
                     A = An;
                 }
                 // positives = slots - negatives (padding and never-voting rows are negative)
 #pragma unroll
                 for (int j = 0; j < kMSet; ++j) cnt[j] += ((hfm >> j) & 1u) ? 8 * nb - (int)(neg[j] / 255u) : 0;
+                { const uint64_t t = cyc(); c_hot += t - c_mark; c_mark = t; }
                 // ---- band pairs: the same MFMA again (bit-identical); each pair
                 // against its own distance, bounded from the MFMA's own forms:
                 // D = |h - c| <= |x'| + |y'| = |X| / tau + |Y| (scaled by s;
                 // the forms' own errors, < gzm B s, add < 1e-3 of G), and the
                 // reference's sequence inside the band ----
 #ifdef PVM_ABL_FIX
-                nfix += __popcll(hitmask);
-                hitmask = 0;
+                nfix += __popcll(hm0) + __popcll(hm1);
+                hm0 = hm1 = 0;
 #endif
                 const float kx = a.gzr / tau * 1.0001f, ky = a.gzr * 1.0001f;
                 // the queued pairs by the reference's sequence, one pair per lane;
@@ -1473,8 +1510,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                     for (int k0 = 0; k0 < nq; k0 += kWave) {
                         if (k0 + lane < nq) {
                             const uint32_t en = bq[k0 + lane];
-                            const int pix = (int)(en & 0xffu), jj = (int)((en >> 8) & 3u), cl = (int)((en >> 10) & 31u);
-                            const int f = (int)(en >> 15) & 1;
+                            const int pix = (int)(en & 0x1ffu), jj = (int)((en >> 9) & 3u), cl = (int)((en >> 11) & 31u);
+                            const int f = (int)(en >> 16) & 1;
                             const F4 e = S.x.get(pix);
                             const float2 hj = hlds[jj * 32 + cl];
                             const int r = exact_vote(e.z, e.w, e.x, e.y, hj.x, hj.y, a.thr) ? 1 : 0;
@@ -1483,9 +1520,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                     }
                     nq = 0;
                 };
-                while (hitmask) {
-                    const int bit = __builtin_ctzll(hitmask);
-                    hitmask &= hitmask - 1;
+                while (hm0 | hm1) {
+                    int bit;
+                    if (hm0) { bit = __builtin_ctzll(hm0); hm0 &= hm0 - 1; }
+                    else { bit = 64 + __builtin_ctzll(hm1); hm1 &= hm1 - 1; }
                     const int p = bit / kMSet, j = bit % kMSet;
                     ++nfix;
                     h4f bj = bf[0];
@@ -1509,7 +1547,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                         if (m) {
                             if (nq > kMQueue - kWave) flush();
                             const int at = nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                            if (u) bq[at] = (uint32_t)pix | ((uint32_t)j << 8) | ((uint32_t)col << 10) | ((signbit(zq) ? 0u : 1u) << 15);
+                            if (u) bq[at] = (uint32_t)pix | ((uint32_t)j << 9) | ((uint32_t)col << 11) | ((signbit(zq) ? 0u : 1u) << 16);
                             nq += __popcll(m);
                         }
                     }
@@ -1530,7 +1568,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                         const float2 hx2 = hlds[j * 32 + l];
                         int c = 0;
 #pragma unroll
-                        for (int k = 0; k < kVoteChunk / kWave; ++k) {
+                        for (int k = 0; k < kMChunk / kWave; ++k) {
                             const int jj = k * kWave + lane;
                             bool e = false;
                             if (jj < np) {
@@ -1568,6 +1606,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
         }
         lo += te - ts;
         ++nseg;
+        { const uint64_t t = cyc(); c_fix += t - c_mark; c_mark = t; }
+    }
+    if (a.trace && lane == 0) {
+        const int wave = (int)(blockIdx.x * 4 + wid);
+        uint64_t *q = a.trace + 65536 + wave * 4;
+        q[0] = c_seg; q[1] = c_stage; q[2] = c_hot; q[3] = c_fix;
     }
     if (a.trace && lane == 0) {
         const int wave = (int)(blockIdx.x * 4 + wid);

@@ -27,7 +27,7 @@ L.pv_debug_set_vote_trace(ctypes.c_void_p(buf.data_ptr()))
 ransac_voting_layer_v3_from_network(seg, vert, 512)
 torch.cuda.synchronize()
 L.pv_debug_set_vote_trace(None)
-t = buf.view(-1, 8).cpu().numpy()
+t = buf[:65536].view(-1, 8).cpu().numpy()
 t = t[t[:, 0] > 0]
 s, e, hw = t[:, 0], t[:, 1], t[:, 2]
 nfix, nseg = t[:, 3] & 0xffffffff, t[:, 3] >> 32
@@ -104,7 +104,16 @@ print("end after the SIMD's first end, by start rank:",
 slot = hw & 0xF
 print("end after the SIMD's first end, by wave slot:",
       [f"{k}: {erel[slot == k].mean():.2f}" for k in np.unique(slot)])
-blk = np.nonzero(buf.view(-1, 8).cpu().numpy()[:, 0] > 0)[0] // 4
+blk = np.nonzero(buf[:65536].view(-1, 8).cpu().numpy()[:, 0] > 0)[0] // 4
 q = np.digitize(blk, np.percentile(blk, [25, 50, 75]))
 print("end by block-index quartile (mean):", [f"{k}: {e_us[q == k].mean():.2f}" for k in range(4)])
 print("corr(end - SIMD first end, fix steps):", np.corrcoef(erel, nfix)[0, 1])
+# per-phase shader cycles (s_memtime) of each wave: segment setup (hypotheses,
+# first loads), sub-chunk staging, hot loop, band fixes + the rest
+ph = buf.cpu().numpy()[65536:65536 + 4 * 16384].reshape(-1, 4)[:len(t)].astype(np.float64)
+if ph.sum() > 0:
+    names = ["seg", "stage", "hot", "fix"]
+    tot = ph.sum(1)
+    print("phase cycles per wave (median):", {n: int(np.median(ph[:, k])) for k, n in enumerate(names)},
+          "total", int(np.median(tot)))
+    print("phase share of all wave cycles:", {n: round(float(ph[:, k].sum() / ph.sum()), 3) for k, n in enumerate(names)})
