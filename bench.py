@@ -514,7 +514,7 @@ def measure_e2e(dev, half=False, batch=1, iters=10, hn=512):
                 voting_ms_per_batch=round((dt - dtb) * 1e3, 4), foreground_px=[int(tn.min()), int(tn.max())],
                 note="random-init weights (none ship with the reference): timing only; images/s covers backbone + "
                      "v3 in one graph; the backbone alone is a separate graph (MIOpen kernels: "
-                     "profiles/r02_backbone_kernel_stats.csv)")
+                     "the MIOpen / CK kernels in profiles/r02_bench_kernel_stats.csv)")
 
 
 def measure_kp_vs_ref(dev):
