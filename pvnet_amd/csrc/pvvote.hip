@@ -1383,7 +1383,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
             if (!(fabsf(ox) <= 1.6e7f && fabsf(oy) <= 1.6e7f)) { ox = 0.f; oy = 0.f; }
             const float axr = fmaxf(cxh - ox, ox - cxl), ayr = fmaxf(cyh - oy, oy - cyl);
             const float R = __builtin_amdgcn_sqrtf(fmaf(axr, axr, ayr * ayr)) * 1.00001f;
-            bool slow = !a.fast || exq != 0 || !(R <= kMRMax);
+            // (the fp16 b operands reach max(tau, 1) R: tau u.c' for X, u x c' for Y)
+            bool slow = !a.fast || exq != 0 || !(R * fmaxf(tau, 1.f) <= kMRMax);
             slow = __builtin_amdgcn_readfirstlane(slow);
             nslow += slow ? 1 : 0;
 #pragma unroll
@@ -2788,6 +2789,353 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5, 8))
 #endif
 }
 
+// --------------------------------------------------------------------------
+// voting_for_hypothesis (dense bytes) on the matrix cores: k_vote_bytes_mfma
+// --------------------------------------------------------------------------
+// The pair's two rotated-frame forms X = tau u.(h'-c'), Y = u x (h'-c') are
+// the same [pixels x 3] by [3 x hypotheses] product as in k_vote_mfma (§5a of
+// fp16 hi/lo-split operands, one v_mfma_f32_32x32x8_f16 per 16
+// pixels x 32 hypotheses); the VALU keeps nz = |Y| - X, the inlier bytes (the
+// sign bits of nz gathered by v_perm) and the band minimum.  The MFMA leaves
+// lane (column c, half k) with 8 pixels of hypothesis c; the A rows are staged
+// so that those are pixels 8k .. 8k+7 of the batch, i.e. 8 contiguous bytes
+// of row c.  They go to a per-wave LDS tile of 32 rows x 128 bytes, band
+// pairs are decided there by the reference's sequence, and the tile leaves as
+// row stores of 16 lanes x 8 bytes (the MFMA's own layout, 32 rows x 16 B per
+// store, measured 2.5x slower than contiguous row segments:
+// tools/store_mfma.hip).
+// Block = 4 waves on one (window of 512 pixels, keypoint); wave = kUSets
+// column sets of 32 hypotheses.  The grid exceeds the resident blocks, so the
+// dispatcher balances the CUs (a later block's staging overlaps the others'
+// matrix work).
+// Measured (tools/u1m_var.sh, rocprof on the U1 call): 39.7-40.2 us against
+// the VALU kernel's 31.3 us -- without stores 30.5-32 us against its 26.4:
+// the matrix-core form does not pay here (K = 16 form 42 us, 4 waves per
+// SIMD with 64-byte tiles 39.8 us, 64 hypotheses per wave 41.1 us), so
+// k_vote_bytes stays the default; PVVOTE_BYTES_MFMA=1 selects this one for
+// A/B runs and the tests check both kernels' bytes.
+constexpr int kUB = 16;                        // pixels per MFMA batch
+constexpr int kUWin = 512;                     // pixels per window (block)
+constexpr int kUBat = kUWin / kUB;             // batches per window (32)
+#ifndef PVU_SUBB
+#define PVU_SUBB 8
+#endif
+constexpr int kUSubB = PVU_SUBB;               // batches per tile
+constexpr int kUSubP = kUSubB * kUB;           // pixels per tile (128)
+constexpr int kUTileRS = kUSubP + 8;           // tile row stride, bytes (34 dwords: conflict-free writes)
+constexpr int kUQueue = 256;                   // band pairs queued per wave
+#ifndef PVU_SETS
+#define PVU_SETS 1
+#endif
+constexpr int kUSets = PVU_SETS;               // 32-hypothesis column sets per wave
+
+struct UArgs {
+    const float *direct;   // [tn][vn][2]
+    const float *coords;   // [tn][2]
+    const float *hypo;     // [hn][vn][2]
+    uint8_t *out;          // [hn][vn][tn]
+    int tn, vn, hn, nwin, nhb, items, per;   // per: items per XCD (0: blockIdx order)
+    float thr, tau, gzm, gzr;
+    int fast, dbg;
+};
+
+__device__ uint64_t *g_utrace;   // debug (pv_debug_set_bytes_utrace): per-wave phase stamps of k_vote_bytes_mfma
+
+#ifndef PVU_WPE
+#define PVU_WPE 3
+#endif
+#ifndef PVU_K16
+#define PVU_K16 0
+#endif
+#if PVU_K16
+typedef _Float16 FragU __attribute__((ext_vector_type(8)));
+#define PVU_MFMA __builtin_amdgcn_mfma_f32_32x32x16_f16
+#else
+typedef h4f FragU;
+#define PVU_MFMA __builtin_amdgcn_mfma_f32_32x32x8f16
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVU_WPE, 8))) void k_vote_bytes_mfma(UArgs a) {
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    __shared__ uint4 arows[kUBat][2 * kUB];                 // A rows [batch][2 m + form], 16 KiB
+    __shared__ float4 rawp[kUWin];                          // the window's (c, d) as given, 8 KiB
+    __shared__ float2 hyp_all[4][kUSets * 32];              // each wave's hypotheses as given
+    __shared__ alignas(16) uint8_t tile_all[4][32 * kUTileRS];   // each wave's 32 x 128 byte tile
+    __shared__ uint32_t q_all[4][kUQueue];                  // each wave's band pairs
+    __shared__ float4 part[4];
+    __shared__ int part_x[4];
+    const int lane = lane_id();
+    const int wid = (int)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int col = lane & 31, half = lane >> 5;
+    int item = (int)blockIdx.x;
+    if (a.per) item = (item % 8) * a.per + item / 8;   // an XCD's blocks: neighbouring items (speed only)
+    if (item >= a.items) return;
+    const int hb = item % a.nhb, rest = item / a.nhb;
+    const int v = uniform(rest % a.vn), w = uniform(rest / a.vn);
+    const int t0 = w * kUWin;
+    const int np = uniform(min(kUWin, a.tn - t0));
+    const int hw0 = (hb * 4 + wid) * (kUSets * 32);          // the wave's first hypothesis
+    float2 *hyp = hyp_all[wid];
+    uint8_t *tile = tile_all[wid];
+    uint32_t *bq = q_all[wid];
+    __builtin_amdgcn_s_setprio(3);
+
+    // ---- loads: the window's pixels (2 per thread), the wave's hypotheses ----
+    float2 c[2], d[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int tt = k * 256 + (int)threadIdx.x;
+        c[k] = d[k] = make_float2(0.f, 0.f);
+        if (tt < np) { c[k] = *(const float2 *)(a.coords + (int64_t)(t0 + tt) * 2);
+                       d[k] = *(const float2 *)(a.direct + ((int64_t)(t0 + tt) * a.vn + v) * 2); }
+    }
+#pragma unroll
+    for (int j = 0; j < kUSets; ++j) {
+        const int h = hw0 + j * 32 + col;
+        if (half == 0) {
+            float2 hv = make_float2(0.f, 0.f);
+            if (h < a.hn) hv = *(const float2 *)(a.hypo + ((int64_t)h * a.vn + v) * 2);
+            hyp[j * 32 + col] = hv;
+        }
+    }
+    // ---- the window's frame: bounding-box centre origin, radius, fast domain ----
+    constexpr float kBig = 3.0e38f;
+    float4 q[2];
+    float xl = kBig, xh = -kBig, yl = kBig, yh = -kBig;
+    bool exo = false;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int tt = k * 256 + (int)threadIdx.x;
+        q[k] = make_float4(__builtin_nanf(""), 0.f, 0.f, 0.f);
+        if (tt < np) {
+            // the reference's norm1 gate (KU:119-121); u = n rsq(n.n), rounded
+            // per component (only its direction matters, as in prep_compacted)
+            bool ex;
+            q[k] = prep_compacted(F4{c[k].x, c[k].y, d[k].x, d[k].y}, &ex);
+            exo |= ex;
+            xl = fminf(xl, c[k].x); xh = fmaxf(xh, c[k].x);
+            yl = fminf(yl, c[k].y); yh = fmaxf(yh, c[k].y);
+            rawp[tt] = make_float4(c[k].x, c[k].y, d[k].x, d[k].y);
+        }
+    }
+    xl = wave_min(xl); xh = wave_max(xh);
+    yl = wave_min(yl); yh = wave_max(yh);
+    const bool wexo = __builtin_amdgcn_ballot_w64(exo) != 0;
+    if (lane == 0) { part[wid] = make_float4(xl, xh, yl, yh); part_x[wid] = wexo; }
+    __syncthreads();
+    float cxl = kBig, cxh = -kBig, cyl = kBig, cyh = -kBig;
+    int exq = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float4 P = part[k];
+        cxl = fminf(cxl, P.x); cxh = fmaxf(cxh, P.y);
+        cyl = fminf(cyl, P.z); cyh = fmaxf(cyh, P.w);
+        exq |= part_x[k];
+    }
+    float ox = floorf(0.5f * cxl + 0.5f * cxh), oy = floorf(0.5f * cyl + 0.5f * cyh);
+    if (!(fabsf(ox) <= 1.6e7f && fabsf(oy) <= 1.6e7f)) { ox = 0.f; oy = 0.f; }
+    const float axr = fmaxf(cxh - ox, ox - cxl), ayr = fmaxf(cyh - oy, oy - cyl);
+    const float R = __builtin_amdgcn_sqrtf(fmaf(axr, axr, ayr * ayr)) * 1.00001f;
+    const float tau = a.tau;
+    // (|b| <= max(tau, 1) R must stay in fp16 range)
+    const bool slow = __builtin_amdgcn_readfirstlane(!a.fast || exq != 0 || !(R * fmaxf(tau, 1.f) <= kMRMax));
+    // ---- A rows: pixel p of batch b at row pair m(p), so that the MFMA hands
+    // lane (column, half k) pixels 8k .. 8k+7 ----
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int tt = k * 256 + (int)threadIdx.x;
+        uint4 rx = make_uint4(0u, 0u, pack_h2((_Float16)0.f, (_Float16)0.f),
+                              pack_h2((_Float16)(-60000.f), (_Float16)0.f));   // never votes: X = -6e4 s
+        uint4 ry = make_uint4(0u, 0u, 0u, 0u);
+        if (q[k].x == q[k].x && !slow) {
+            const float cx = q[k].x - ox, cy = q[k].y - oy;
+            const float axX = tau * q[k].z, ayX = tau * q[k].w;
+            rx = form_row(axX, ayX, fmaf(axX, cx, ayX * cy));
+            ry = form_row(-q[k].w, q[k].z, fmaf(-q[k].w, cx, q[k].z * cy));
+        }
+        const int p = tt & 15, qq = p & 7, m = (qq & 1) + 4 * (qq >> 1) + 2 * (p >> 3);
+        arows[tt >> 4][2 * m] = rx;
+        arows[tt >> 4][2 * m + 1] = ry;
+    }
+    __syncthreads();
+    __builtin_amdgcn_s_setprio(1);
+    const uint64_t t_staged = __builtin_amdgcn_s_memrealtime();
+
+    const float kx = a.gzr / fmaxf(tau, 1e-30f) * 1.0001f, ky = a.gzr * 1.0001f;
+#if PVU_K16
+    // gfx950's K = 16 form: the 8 terms in lane half 0 (k 0..7), zeros in half 1
+    auto afrag = [&](int b) -> FragU {
+        const uint4 r = half ? make_uint4(0u, 0u, 0u, 0u) : arows[b][col];
+        return __builtin_bit_cast(FragU, r);
+    };
+#else
+    const uint2 *arow = (const uint2 *)&arows[0][0];
+    auto afrag = [&](int b) -> FragU { return __builtin_bit_cast(FragU, arow[(b * kUB * 2 + col) * 2 + half]); };
+#endif
+    const f32x16 zero = {};
+    const int64_t rstep = (int64_t)a.vn * a.tn;
+    constexpr uint32_t kSgn01 = 0x0c0c0b09u, kSgn23 = 0x0b090c0cu;   // sign bytes (see vote_bytes_seg)
+    auto pack4 = [](float z0, float z1, float z2, float z3) {
+        const uint32_t p01 = __builtin_amdgcn_perm(__float_as_uint(z1), __float_as_uint(z0), kSgn01);
+        const uint32_t p23 = __builtin_amdgcn_perm(__float_as_uint(z3), __float_as_uint(z2), kSgn23);
+        return (p01 | p23) & 0x01010101u;
+    };
+
+#pragma unroll 1
+    for (int j = 0; j < kUSets; ++j) {
+        const int hc0 = hw0 + j * 32;                   // this set's first hypothesis
+        if (hc0 >= a.hn) break;
+        // ---- B fragment and band of the lane's hypothesis for this frame ----
+        const float2 hv = hyp[j * 32 + col];
+        const int h = hc0 + col;
+        const bool fin = isfinite(hv.x) && isfinite(hv.y);
+        const bool xo = h < a.hn && !slow &&
+                        (!fin || hyp_exact_only(hv.x, hv.y) || !(fabsf(hv.x) < kMHypMax && fabsf(hv.y) < kMHypMax));
+        const bool hf = h < a.hn && !slow && !xo;
+        const uint32_t xcols = (uint32_t)__builtin_amdgcn_ballot_w64(xo && half == 0);
+        FragU bf = {};
+        float gb = -1.f, G = 0.f;
+        {
+            const float hx = hv.x - ox, hy = hv.y - oy;
+            const float mag = fmaxf(fabsf(hx), fabsf(hy));
+            const int e = __builtin_amdgcn_frexp_expf(mag);
+            const int k = hf ? max(0, e - 14) : 0;
+            const float s = __builtin_ldexpf(1.f, -k);
+            const float hxs = hx * s, hys = hy * s;
+            const _Float16 xh_ = (_Float16)hxs, xl_ = (_Float16)(hxs - (float)xh_);
+            const _Float16 yh_ = (_Float16)hys, yl_ = (_Float16)(hys - (float)yh_);
+            const _Float16 sh = (_Float16)s;
+            if (hf) {
+#if PVU_K16
+                if (!half) bf = FragU{xh_, xl_, xh_, yh_, yl_, yh_, sh, sh};
+#else
+                bf = half ? FragU{yl_, yh_, sh, sh} : FragU{xh_, xl_, xh_, yh_};
+#endif
+                const float Bv = (__builtin_amdgcn_sqrtf(fmaf(hx, hx, hy * hy)) * 1.00001f + R) * 1.00001f + 1.f;
+                gb = (a.gzm + a.gzr) * Bv * s * 1.00001f;
+                G = a.gzm * Bv * s * 1.001f;
+            }
+        }
+        // lane's store pointer: row hc0 + kRPS r + srow, bytes 8 sl of a tile row
+        constexpr int kLPR = kUSubP / 8, kRPS = kWave / kLPR;   // lanes per tile row, rows per store
+        const int srow = lane / kLPR, sl = lane % kLPR;
+        uint8_t *sp = a.out + ((int64_t)(hc0 + srow) * a.vn + v) * a.tn + t0 + 8 * sl;
+#pragma unroll 1
+        for (int sc = 0; sc * kUSubP < np; ++sc) {
+            const int pb = sc * kUSubP;                  // the tile's first pixel in the window
+            uint32_t hm = 0;
+            if (!slow) {
+                // ---- hot loop: 8 MFMAs, inlier bytes into the tile, band ballots ----
+                FragU A = afrag(sc * kUSubB);
+                f32x16 cc = PVU_MFMA(A, bf, zero, 0, 0, 0);
+#pragma unroll
+                for (int p = 0; p < kUSubB; ++p) {
+                    f32x16 cn = cc;
+                    if (p + 1 < kUSubB) cn = PVU_MFMA(afrag(sc * kUSubB + p + 1), bf, zero, 0, 0, 0);
+                    float nz[8];
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) nz[r] = fabsf(cc[2 * r + 1]) - cc[2 * r];
+                    const uint32_t lo = pack4(nz[0], nz[1], nz[2], nz[3]);
+                    const uint32_t hi = pack4(nz[4], nz[5], nz[6], nz[7]);
+                    *(uint2 *)(tile + col * kUTileRS + 16 * p + 8 * half) = make_uint2(lo, hi);
+                    float mb = __builtin_elementwise_minimum(__builtin_elementwise_minimum(fabsf(nz[0]), fabsf(nz[1])), fabsf(nz[2]));
+                    mb = __builtin_elementwise_minimum(__builtin_elementwise_minimum(mb, fabsf(nz[3])), fabsf(nz[4]));
+                    mb = __builtin_elementwise_minimum(__builtin_elementwise_minimum(mb, fabsf(nz[5])), fabsf(nz[6]));
+                    mb = __builtin_elementwise_minimum(mb, fabsf(nz[7]));
+                    hm |= __builtin_amdgcn_ballot_w64(mb <= gb) != 0 ? 1u << p : 0u;
+                    cc = cn;
+                }
+                if (a.dbg == 5) hm = 0;   // profiling ablation only (PVVOTE_DEBUG_BYTES=5: wrong bytes)
+                // ---- band: the flagged MFMAs again (bit-identical), each pair
+                // against its own bound (D <= |X|/tau + |Y|, as k_vote_mfma);
+                // inside it the reference's sequence decides the tile byte ----
+                int nq = 0;
+                auto flush = [&]() {
+                    for (int k0 = 0; k0 < nq; k0 += kWave) {
+                        if (k0 + lane < nq) {
+                            const uint32_t en = bq[k0 + lane];
+                            const int pix = (int)(en & 0x1ffu), cl = (int)(en >> 9);
+                            const float4 e = rawp[pix];
+                            const float2 hj = hyp[j * 32 + cl];
+                            tile[cl * kUTileRS + (pix - pb)] = exact_vote(e.z, e.w, e.x, e.y, hj.x, hj.y, a.thr) ? 1 : 0;
+                        }
+                    }
+                    nq = 0;
+                };
+                while (hm) {
+                    const int p = __builtin_ctz(hm);
+                    hm &= hm - 1;
+                    const f32x16 cb = PVU_MFMA(afrag(sc * kUSubB + p), bf, zero, 0, 0, 0);
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+                        const float X = cb[2 * r], Y = cb[2 * r + 1];
+                        const float zq = X - fabsf(Y);
+                        const float g = fmaf(kx, fabsf(X), fmaf(ky, fabsf(Y), G));
+                        const int pix = pb + kUB * p + 8 * half + r;
+                        const bool u = hf && pix < np && fabsf(zq) <= g;
+                        const uint64_t m = __builtin_amdgcn_ballot_w64(u);
+                        if (m) {
+                            if (nq > kUQueue - kWave) flush();
+                            const int at = nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                            if (u) bq[at] = (uint32_t)pix | ((uint32_t)col << 9);
+                            nq += __popcll(m);
+                        }
+                    }
+                }
+                flush();
+            }
+            // ---- exact-only hypotheses (rare), or every pair of a slow window:
+            // lane = pixel, one hypothesis column at a time ----
+            uint32_t xc = slow ? 0xffffffffu : xcols;
+            while (xc) {
+                const int l = __builtin_ctz(xc);
+                xc &= xc - 1;
+                if (hc0 + l >= a.hn) break;
+                const float2 hj = hyp[j * 32 + l];
+#pragma unroll
+                for (int k = 0; k < kUSubP / kWave; ++k) {
+                    const int pl = k * kWave + lane, pix = pb + pl;
+                    bool e = false;
+                    if (pix < np) {
+                        const float4 r = rawp[pix];
+                        e = exact_vote(r.z, r.w, r.x, r.y, hj.x, hj.y, a.thr);
+                    }
+                    tile[l * kUTileRS + pl] = e ? 1 : 0;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            // ---- the tile's rows: 4 rows x 128 bytes per store ----
+            const bool full = t0 + pb + kUSubP <= a.tn;
+#pragma unroll
+            for (int r = 0; r < 32 / kRPS; ++r) {
+                const int row = kRPS * r + srow;
+                const uint2 x = *(const uint2 *)(tile + row * kUTileRS + 8 * sl);
+                if (hc0 + row < a.hn && a.dbg != 6) {   // (6: profiling ablation, no stores)
+                    uint8_t *p = sp + rstep * (kRPS * r) + pb;
+                    typedef uint64_t u64a1 __attribute__((aligned(1)));
+                    const int t = t0 + pb + 8 * sl;
+                    if (full || t + 8 <= a.tn) {
+                        *(u64a1 *)p = (uint64_t)x.y << 32 | x.x;
+                    } else {
+                        uint64_t y = (uint64_t)x.y << 32 | x.x;
+                        for (int k = 0; k < 8 && t + k < a.tn; ++k) { p[k] = (uint8_t)y; y >>= 8; }
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if (g_utrace && lane == 0) {
+        uint64_t *tr = g_utrace + ((int64_t)blockIdx.x * 4 + wid) * 4;
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        tr[0] = t_start;
+        tr[1] = t_staged;
+        tr[2] = __builtin_amdgcn_s_memrealtime();
+        tr[3] = ((uint64_t)xcc << 32) | hw;
+    }
+}
+
 // test hook of wave_min / wave_max (pv_debug_wave_minmax)
 __global__ __launch_bounds__(64) void k_debug_minmax(const float *in, float *out) {
     const float x = in[blockIdx.x * 64 + threadIdx.x];
@@ -2920,11 +3268,12 @@ uint64_t *g_vote_trace = nullptr;   // debug hook (pv_debug_set_vote_trace)
 // A/B and debug knobs of pv_voting_for_hypothesis, read from the environment
 // once per process (never per call, so graph captures and eager calls agree)
 struct ByteKnobs {
-    int dbg = 0, wpb = 4, xcd = 1, nobal = 0;
+    int dbg = 0, wpb = 4, xcd = 1, nobal = 0, mfma = 0;   // mfma: k_vote_bytes_mfma (A/B only)
 };
 ByteKnobs &byte_knobs() {
     static ByteKnobs k = [] {
         ByteKnobs r;
+        if (const char *e = getenv("PVVOTE_BYTES_MFMA")) r.mfma = atoi(e);
         if (const char *e = getenv("PVVOTE_DEBUG_BYTES")) r.dbg = atoi(e);
         if (const char *e = getenv("PVVOTE_BYTES_WPB")) r.wpb = atoi(e) == 1 ? 1 : 4;
         if (const char *e = getenv("PVVOTE_BYTES_XCD")) r.xcd = atoi(e);
@@ -3213,6 +3562,26 @@ int pv_voting_for_hypothesis(const float *direct, const float *coords, const flo
     ba.nhg = (hn + kByteHB - 1) / kByteHB;
     const ByteKnobs &kn = byte_knobs();
     ba.dbg = kn.dbg;
+    if (mode == PV_VOTE_DENSE && kn.mfma) {
+        // the matrix-core kernel (k_vote_bytes_mfma): one block per (window,
+        // keypoint, 4 x kUSets x 32 hypotheses), XCD-grouped item order
+        UArgs ua{};
+        ua.direct = direct; ua.coords = coords; ua.hypo = hypo; ua.out = inliers;
+        ua.tn = tn; ua.vn = vn; ua.hn = hn;
+        ua.nwin = (tn + kUWin - 1) / kUWin;
+        ua.nhb = (hn + 4 * kUSets * 32 - 1) / (4 * kUSets * 32);
+        const int64_t uitems = (int64_t)ua.nwin * vn * ua.nhb;
+        if (uitems >= (1ll << 31) - 8) return PV_EINVAL;
+        ua.items = (int)uitems;
+        ua.per = kn.xcd ? (int)((uitems + 7) / 8) : 0;
+        ua.thr = fc.thr; ua.tau = fc.tau; ua.fast = fc.fast;
+        ua.gzm = fc.fast ? mfma_gz(fc.tau) : 0.f;
+        ua.gzr = fc.gzr;
+        ua.dbg = kn.dbg;
+        const unsigned ugrid = (unsigned)(ua.per ? 8 * (int64_t)ua.per : uitems);
+        k_vote_bytes_mfma<<<ugrid, 256, 0, (hipStream_t)stream>>>(ua);
+        return last();
+    }
     const int64_t items = (int64_t)vn * ba.nwin * ba.nhg;
     if (items >= (1ll << 31)) return PV_EINVAL;   // the kernel's 32-bit item index
     // one launch, no scratch: the operands are made where the blocks stage them
@@ -3309,6 +3678,14 @@ int pv_debug_set_vote_kernel(int32_t which) {
     return prev;
 }
 // test hook: the byte kernel's debug mode (PVVOTE_DEBUG_BYTES) at run time; returns the previous one
+// debug: per-wave stamps of k_vote_bytes_mfma into buf (4 x u64 per wave; nullptr: off)
+int pv_debug_set_bytes_utrace(uint64_t *buf) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_utrace), &buf, sizeof(buf)); }
+// test hook: the dense byte kernel (1: k_vote_bytes_mfma, 0: k_vote_bytes); returns the previous
+int pv_debug_set_bytes_mfma(int32_t on) {
+    const int prev = byte_knobs().mfma;
+    byte_knobs().mfma = on;
+    return prev;
+}
 int pv_debug_set_bytes_mode(int32_t dbg) {
     const int prev = byte_knobs().dbg;
     byte_knobs().dbg = dbg;

@@ -72,8 +72,21 @@ def test_wave_min_max_reduction(device):
 
 
 # ---------------------------------------------------------------- kernels
+@pytest.fixture(params=["mfma", "valu"])
+def bytes_kernel(request):
+    """Both dense byte kernels in one process: the VALU k_vote_bytes (the
+    default) and the matrix-core k_vote_bytes_mfma (A/B option), switched by
+    pv_debug_set_bytes_mfma (a test-only export)."""
+    L = _lib.load()
+    L.pv_debug_set_bytes_mfma.argtypes = [ctypes.c_int32]
+    L.pv_debug_set_bytes_mfma.restype = ctypes.c_int32
+    prev = L.pv_debug_set_bytes_mfma(1 if request.param == "mfma" else 0)
+    yield request.param
+    L.pv_debug_set_bytes_mfma(prev)
+
+
 @pytest.mark.parametrize("case", ["cat_v3_512", "synth_v3_512"])
-def test_generate_and_vote_kernels_bit_exact(case, device, rv):
+def test_generate_and_vote_kernels_bit_exact(case, device, rv, bytes_kernel):
     g = G.load(case)
     mask, vertex = (G.cat_inputs(g) if case.startswith("cat") else G.synth_inputs(g))[:2]
     coords, direct = O.compact(O.fg_mask_v3(mask[0]), vertex[0])
@@ -94,7 +107,7 @@ def test_generate_and_vote_kernels_bit_exact(case, device, rv):
         np.testing.assert_array_equal(out.cpu().numpy().sum(2), g["counts"][0][hs])
 
 
-def test_vote_bytes_full_size(device, rv):
+def test_vote_bytes_full_size(device, rv, bytes_kernel):
     """The bench's U1 call (hn=512, tn=29,861: the CU-balanced grid of full
     and quarter blocks): every row's inliers sum to the golden counts, and
     sampled rows -- in full blocks and in quarter blocks -- equal the
@@ -114,7 +127,7 @@ def test_vote_bytes_full_size(device, rv):
         np.testing.assert_array_equal(out[torch.from_numpy(rows).to(device)].cpu().numpy(), ref)
 
 
-def test_vote_bytes_balanced_grid_other_shape(device, rv):
+def test_vote_bytes_balanced_grid_other_shape(device, rv, bytes_kernel):
     """hn=256, tn=15,000 (270 units on 256 CUs: 256 full + 56 quarter blocks,
     a different split of the CU-balanced grid): row sums equal the fused
     vote-count kernel's counts, sampled rows equal the oracle's bytes."""
@@ -148,7 +161,7 @@ def test_voting_or_semantics_keeps_existing_bytes(device, rv):
 
 
 @pytest.mark.parametrize("seed", [0, 1, 2])
-def test_guard_band_stress(seed, device, rv):
+def test_guard_band_stress(seed, device, rv, bytes_kernel):
     """Thresholds placed exactly on reference cosines, degenerate pixels and
     hypotheses: every byte must still equal the exact reference decision."""
     rng = np.random.default_rng(seed)
@@ -175,8 +188,35 @@ def test_guard_band_stress(seed, device, rv):
         np.testing.assert_array_equal(cnt, ref.sum(2), err_msg=f"thr={thr}")
 
 
+@pytest.mark.parametrize("span", [5000.0, 40000.0])
+def test_vote_bytes_wide_frames(span, device, rv, bytes_kernel):
+    """API coordinates spread over thousands of pixels at low thresholds: the
+    matrix-core kernel's fp16 operands (b = tau u.c' up to tau R) must stay in
+    range, or the window takes the exact sequence; fractional coordinates,
+    a partial last window and a partial hypothesis set (hn = 80)."""
+    rng = np.random.default_rng(int(span))
+    tn, vn, hn = 1500, 2, 80
+    coords = (rng.random((tn, 2)) * span).astype(np.float32)
+    coords[::3] = np.round(coords[::3])
+    ang = rng.uniform(-np.pi, np.pi, (tn, vn))
+    direct = np.stack([np.cos(ang), np.sin(ang)], -1).astype(np.float32)
+    hyp = (rng.random((hn, vn, 2)) * span * 1.2 - span * 0.1).astype(np.float32)
+    for thr in (0.3, 0.9, 0.99):
+        ref = np.zeros((hn, vn, tn), np.uint8)
+        O.voting_for_hypothesis(direct, coords, hyp, ref, thr)
+        assert 0 < ref.sum() < ref.size
+        out = torch.full(ref.shape, 9, dtype=torch.uint8, device=device)
+        rv.voting_for_hypothesis_dense(cu(direct, device), cu(coords, device), cu(hyp, device), out, thr)
+        np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"thr={thr}")
+    # the counts at hn = 512 (k_vote_mfma's grid), same frames and thresholds
+    hyp5 = (rng.random((512, vn, 2)) * span * 1.2 - span * 0.1).astype(np.float32)
+    for thr in (0.3, 0.9):
+        cnt = rv.vote_counts(cu(direct, device), cu(coords, device), cu(hyp5, device), thr).cpu().numpy()
+        np.testing.assert_array_equal(cnt, O.vote_counts(direct, coords, hyp5, thr), err_msg=f"counts thr={thr}")
+
+
 @pytest.mark.parametrize("full_queue", [False, True])
-def test_band_pairs_both_modes(full_queue, device, rv):
+def test_band_pairs_both_modes(full_queue, device, rv, bytes_kernel):
     """Band pairs go through k_fix_bytes' queue (or, with the queue full, the
     in-kernel exact pass): dense and OR modes, thresholds on reference cosines."""
     L = _lib.load()
