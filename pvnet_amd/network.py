@@ -139,3 +139,40 @@ class PVNet(nn.Module):
 
 Resnet18_8s = PVNet
 PVnet = PVNet
+
+
+def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d) -> nn.Conv2d:
+    """conv followed by eval-mode bn as one convolution with a bias: per output
+    channel k, w'_k = w_k g_k and b'_k = beta_k + (b_k - mean_k) g_k with
+    g_k = gamma_k / sqrt(var_k + eps) (folded in fp64, stored in conv's dtype)."""
+    g = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
+    b0 = conv.bias.double() if conv.bias is not None else torch.zeros_like(g)
+    out = nn.Conv2d(conv.in_channels, conv.out_channels, conv.kernel_size, conv.stride, conv.padding,
+                    conv.dilation, conv.groups, bias=True, padding_mode=conv.padding_mode,
+                    device=conv.weight.device, dtype=conv.weight.dtype)
+    out.weight.copy_((conv.weight.double() * g.view(-1, 1, 1, 1)).to(conv.weight.dtype))
+    out.bias.copy_((bn.bias.double() + (b0 - bn.running_mean.double()) * g).to(conv.weight.dtype))
+    return out
+
+
+@torch.no_grad()
+def fold_batchnorm(net: nn.Module) -> nn.Module:
+    """Inference copy of a PVNet with every BatchNorm2d folded into the
+    convolution before it (the BN becomes ``nn.Identity``): 25 fewer
+    normalisation passes over the activations per forward, the same function
+    up to rounding.  Load a checkpoint into :class:`PVNet` first (the folded
+    copy's state-dict keys differ); the copy is eval-only."""
+    import copy
+    net = copy.deepcopy(net).eval()
+    for m in list(net.modules()):
+        if isinstance(m, BasicBlock):
+            m.conv1, m.bn1 = _fold(m.conv1, m.bn1), nn.Identity()
+            m.conv2, m.bn2 = _fold(m.conv2, m.bn2), nn.Identity()
+        elif isinstance(m, ResNet18OS8):
+            m.conv1, m.bn1 = _fold(m.conv1, m.bn1), nn.Identity()
+        elif isinstance(m, nn.Sequential):
+            for i in range(len(m) - 1):
+                if isinstance(m[i], nn.Conv2d) and isinstance(m[i + 1], nn.BatchNorm2d):
+                    m[i], m[i + 1] = _fold(m[i], m[i + 1]), nn.Identity()
+    assert not any(isinstance(m, nn.BatchNorm2d) for m in net.modules()), "a BatchNorm2d was left unfolded"
+    return net

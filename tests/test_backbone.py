@@ -21,7 +21,7 @@ import numpy as np
 import pytest
 import torch
 
-from pvnet_amd.network import PVNet
+from pvnet_amd.network import PVNet, fold_batchnorm
 from tests import backbone_init as BI
 from tests.golden_io import load
 
@@ -103,3 +103,33 @@ def test_forward_device_fp16_channels_last_matches_reference(device):
     print(f"fp16 device: max dev {ds:.3e} / {dv:.3e} of scale {sc:.2f} (reference fp16 on CPU: "
           f"{float(G['f16_cpu_max_dev']):.3e})")
     assert ds <= 1.5e-2 * sc and dv <= 1.5e-2 * sc
+
+
+def test_folded_batchnorm_cpu_matches_reference():
+    """fold_batchnorm (the bench's inference form): the seeded G4 weights
+    carry non-trivial BN statistics; the folded forward equals the
+    reference's outputs to 2e-5 of the scale (folding re-rounds the weights)."""
+    net = fold_batchnorm(_net())
+    assert sum(isinstance(m, torch.nn.BatchNorm2d) for m in _net().modules()) == 25
+    with torch.no_grad():
+        seg, ver = net(torch.from_numpy(G["x_small"]))
+    sc = _scale()
+    assert np.abs(seg.numpy() - G["seg_small"]).max() <= 2e-5 * sc
+    assert np.abs(ver.numpy() - G["ver_small"]).max() <= 2e-5 * sc
+
+
+@pytest.mark.gpu
+def test_folded_batchnorm_device_fp16_channels_last_matches_reference(device):
+    """The configs[2] backbone as the bench runs it: BN folded, fp16,
+    channels_last, on MIOpen -- within the same 1.5e-2 of scale as unfolded."""
+    net = fold_batchnorm(_net()).to(device=device, dtype=torch.float16).to(memory_format=torch.channels_last)
+    x = torch.from_numpy(G["x_small"]).to(device).half().contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        seg, ver = net(x)
+        fseg, fver = fold_batchnorm(_net(device=device))(torch.from_numpy(BI.frame_input()).to(device))
+    sc = _scale()
+    ds = np.abs(seg.float().cpu().numpy() - G["seg_small"]).max()
+    dv = np.abs(ver.float().cpu().numpy() - G["ver_small"]).max()
+    print(f"folded fp16 device: max dev {ds:.3e} / {dv:.3e} of scale {sc:.2f}")
+    assert ds <= 1.5e-2 * sc and dv <= 1.5e-2 * sc
+    _frame_check(fseg.cpu().numpy(), fver.cpu().numpy(), 2e-4)
