@@ -453,7 +453,7 @@ FP32_MATRIX_TFLOPS = 157.3           # f32 MFMA = the vector peak (MI355X_MICROA
 BACKBONE_GFLOP = 144.9               # ResNet-18 OS8 seg+vertex forward at 480x640
 
 
-def measure_e2e(dev, half=False, batch=1, iters=30, hn=512):
+def measure_e2e(dev, half=False, batch=1, iters=30, hn=512, form=None):
     """configs[1] (fp32, batch 1) / configs[2] (fp16 backbone, batch 32):
     the ResNet-18 seg+vector-field forward (PyTorch-ROCm, MIOpen,
     channels_last) and the HIP v3 layer on the network's own outputs (fp16
@@ -464,17 +464,22 @@ def measure_e2e(dev, half=False, batch=1, iters=30, hn=512):
     predicts, so this times the path, not accuracy.  The backbone alone is
     timed too (its own graph) for its fraction of the matrix peak."""
     from pvnet_amd import ransac_voting_gpu as rvg
-    from pvnet_amd.network import PVNet, fold_batchnorm
+    from pvnet_amd.network import PVNet, PVNetInference, fold_batchnorm
     torch.backends.cudnn.benchmark = True      # MIOpen: search the convolution algorithms once
     torch.manual_seed(0)
     dt_ = torch.float16 if half else torch.float32
-    # fp16 batch 32: BatchNorm folded into the convolutions (fold_batchnorm,
-    # parity-tested against G4): backbone 16.9 -> 14.5 ms, 1.81k -> 2.10k
-    # images/s (tools/e2e_ab.py, interleaved); fp32 batch 1 measured 1.4 %
-    # slower folded (the bias pass costs what the BN pass did), so it keeps BN
+    # fp16 batch 32: PVNetInference -- BatchNorm folded into the convolutions
+    # (backbone 16.9 -> 14.5 ms) and each decoder upsampling fused with the
+    # cat after it in one HIP pass (pv_upsample2x_cat_f16); both parity-tested
+    # against G4 (tools/e2e_ab.py: interleaved A/B of the forms).  fp32 batch 1
+    # measured 1.4 % slower folded (the bias pass costs what the BN pass did),
+    # so it runs the plain module.
+    form = form or ("inference" if half else "plain")
     net = PVNet(18, 2).eval()
-    if half:
+    if form == "folded":
         net = fold_batchnorm(net)
+    elif form == "inference":
+        net = PVNetInference(net)
     net = net.to(dev).to(dtype=dt_, memory_format=torch.channels_last)
     x = torch.randn(batch, 3, H, W, device=dev).to(dtype=dt_, memory_format=torch.channels_last)
     ws = rvg.VotingWorkspace()
@@ -517,13 +522,13 @@ def measure_e2e(dev, half=False, batch=1, iters=30, hn=512):
     peak = FP16_MFMA_DENSE_TFLOPS if half else FP32_MATRIX_TFLOPS
     bb_tf = BACKBONE_GFLOP * batch / dtb / 1e3
     return dict(images_per_s=round(batch / dt, 1), ms_per_batch=round(dt * 1e3, 4), batch=batch,
-                backbone_dtype="float16" if half else "float32", voting_dtype="float32", backbone_bn_folded=bool(half),
+                backbone_dtype="float16" if half else "float32", voting_dtype="float32", backbone_form=form,
                 backbone_ms_per_batch=round(dtb * 1e3, 4), backbone_gflop_per_image=BACKBONE_GFLOP,
                 backbone_tflops=round(bb_tf, 1), backbone_matrix_peak_tflops=peak,
                 backbone_frac_of_matrix_peak=round(bb_tf / peak, 4),
                 voting_ms_per_batch=round((dt - dtb) * 1e3, 4), foreground_px=[int(tn.min()), int(tn.max())],
                 note="random-init weights (none ship with the reference): timing only; images/s covers backbone + "
-                     "v3 in one graph; fp16: BatchNorm folded into the convolutions (pvnet_amd.network.fold_batchnorm); the backbone alone is a separate graph (MIOpen kernels: "
+                     "v3 in one graph; backbone_form inference = pvnet_amd.network.PVNetInference (BN folded, HIP upsample+cat); the backbone alone is a separate graph (MIOpen kernels: "
                      "the MIOpen / CK kernels in profiles/r02_bench_kernel_stats.csv)")
 
 

@@ -204,6 +204,17 @@ int pv_uncertainty_pnp(const pv_pnp_batch *batch, double *Rt, const pv_pnp_diag 
 int pv_uncertainty_pnp_refine(const pv_pnp_batch *batch, const double *init_rt, double *result_rt,
                               const pv_pnp_diag *diag, pv_stream_t stream);
 
+/* ---- the network's decoder (the ResNet-18 seg + vector-field forward, A8) ---- */
+
+/* replaces nn.UpsamplingBilinear2d(scale_factor=2) followed by torch.cat([up(fm), skip], 1)
+ * (lib/networks/model_repository.py:35-51 modules, :66-75 forward) for channels-last fp16 maps, fused
+ * into one pass, with channels [c1 + c2, cpad) of the output zero (a pad for the convolution after it).
+ * x: [n][hin][win][c1] fp16 (a channels_last NCHW tensor's memory), skip: [n][2 hin][2 win][c2] (may be
+ * NULL when c2 = 0), out: [n][2 hin][2 win][cpad].  c1 and cpad multiples of 8, cpad >= c1 + c2, x and
+ * out 16-byte aligned.  The blend is ATen's upsample_bilinear2d (align_corners=True) arithmetic in f32. */
+int pv_upsample2x_cat_f16(const void *x, const void *skip, void *out, int32_t n, int32_t hin, int32_t win,
+                          int32_t c1, int32_t c2, int32_t cpad, pv_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -176,3 +176,59 @@ def fold_batchnorm(net: nn.Module) -> nn.Module:
                     m[i], m[i + 1] = _fold(m[i], m[i + 1]), nn.Identity()
     assert not any(isinstance(m, nn.BatchNorm2d) for m in net.modules()), "a BatchNorm2d was left unfolded"
     return net
+
+
+def upsample2x_cat(fm: torch.Tensor, skip: torch.Tensor | None, cpad: int) -> torch.Tensor:
+    """``torch.cat([UpsamplingBilinear2d(2)(fm), skip], 1)`` zero-padded to
+    ``cpad`` channels, for channels-last fp16 device tensors, in one HIP pass
+    (``pv_upsample2x_cat_f16``, pvnet_amd/csrc/pvdecoder.hip)."""
+    from pvnet_amd import _lib
+    n, c1, h, w = fm.shape
+    c2 = 0 if skip is None else skip.shape[1]
+    cl = torch.channels_last
+    if fm.dtype != torch.float16 or not fm.is_cuda or not fm.is_contiguous(memory_format=cl):
+        raise RuntimeError("upsample2x_cat: fm must be a channels_last float16 CUDA tensor")
+    if skip is not None and (skip.dtype != torch.float16 or not skip.is_contiguous(memory_format=cl)
+                             or tuple(skip.shape) != (n, c2, 2 * h, 2 * w)):
+        raise RuntimeError("upsample2x_cat: skip must be channels_last float16 [n, c2, 2h, 2w]")
+    out = torch.empty((n, cpad, 2 * h, 2 * w), dtype=torch.float16, device=fm.device, memory_format=cl)
+    stream = torch.cuda.current_stream(fm.device).cuda_stream
+    _lib.check(_lib.load().pv_upsample2x_cat_f16(fm.data_ptr(), None if skip is None else skip.data_ptr(),
+                                                 out.data_ptr(), n, h, w, c1, c2, cpad, stream),
+               "pv_upsample2x_cat_f16")
+    return out
+
+
+class PVNetInference(nn.Module):
+    """fp16 channels-last inference form of a :class:`PVNet` (configs[2]'s
+    backbone): BatchNorm folded into the convolutions (:func:`fold_batchnorm`),
+    each decoder upsampling fused with the concatenation after it
+    (:func:`upsample2x_cat`, one HIP pass instead of two), and the last
+    concatenation (32 + 3 channels) zero-padded to 40 channels with ``convraw``'s
+    first convolution given 5 zero input channels -- the same function up to
+    rounding (MR:64-79).  Input: a channels_last float16 CUDA batch."""
+
+    RAW_PAD = 40
+
+    def __init__(self, net: PVNet):
+        super().__init__()
+        f = fold_batchnorm(net)
+        self.seg_dim = f.seg_dim
+        self.resnet18_8s, self.conv8s, self.conv4s, self.conv2s = f.resnet18_8s, f.conv8s, f.conv4s, f.conv2s
+        c0 = f.convraw[0]
+        pad = nn.Conv2d(self.RAW_PAD, c0.out_channels, c0.kernel_size, c0.stride, c0.padding, bias=True,
+                        device=c0.weight.device, dtype=c0.weight.dtype)
+        with torch.no_grad():
+            pad.weight.zero_()
+            pad.weight[:, :c0.in_channels] = c0.weight
+            pad.bias.copy_(c0.bias)
+        self.convraw = nn.Sequential(pad, *list(f.convraw)[1:])
+        self.eval()
+
+    def forward(self, x):
+        x2s, x4s, x8s, _, _, xfc = self.resnet18_8s(x)
+        fm = self.conv8s(torch.cat([xfc, x8s], 1))
+        fm = self.conv4s(upsample2x_cat(fm, x4s, fm.shape[1] + x4s.shape[1]))
+        fm = self.conv2s(upsample2x_cat(fm, x2s, fm.shape[1] + x2s.shape[1]))
+        x = self.convraw(upsample2x_cat(fm, x, self.RAW_PAD))
+        return x[:, :self.seg_dim], x[:, self.seg_dim:]

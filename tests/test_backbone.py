@@ -21,7 +21,7 @@ import numpy as np
 import pytest
 import torch
 
-from pvnet_amd.network import PVNet, fold_batchnorm
+from pvnet_amd.network import PVNet, PVNetInference, fold_batchnorm, upsample2x_cat
 from tests import backbone_init as BI
 from tests.golden_io import load
 
@@ -133,3 +133,57 @@ def test_folded_batchnorm_device_fp16_channels_last_matches_reference(device):
     print(f"folded fp16 device: max dev {ds:.3e} / {dv:.3e} of scale {sc:.2f}")
     assert ds <= 1.5e-2 * sc and dv <= 1.5e-2 * sc
     _frame_check(fseg.cpu().numpy(), fver.cpu().numpy(), 2e-4)
+
+
+def test_inference_form_construction():
+    """PVNetInference: convraw's first convolution is the folded one with 5
+    zero input channels appended (the 35 -> 40 channel pad of the fused
+    upsample + cat); no BatchNorm left."""
+    net = _net()
+    inf = PVNetInference(net)
+    ref = fold_batchnorm(net).convraw[0]
+    w = inf.convraw[0].weight
+    assert w.shape == (32, 40, 3, 3)
+    assert torch.equal(w[:, :35], ref.weight) and not w[:, 35:].any()
+    assert torch.equal(inf.convraw[0].bias, ref.bias)
+    assert not any(isinstance(m, torch.nn.BatchNorm2d) for m in inf.modules())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c1,c2,cpad,h,w", [(32, 3, 40, 12, 16), (64, 64, 128, 7, 9), (128, 64, 192, 5, 6),
+                                            (16, 0, 24, 3, 4)])
+def test_upsample2x_cat_matches_torch(c1, c2, cpad, h, w, device):
+    """The fused HIP decoder step equals ATen's UpsamplingBilinear2d + cat +
+    zero pad on channels_last fp16 (the same f32 blend; at most one fp16 ulp
+    where the two compilers associate or contract differently)."""
+    g = torch.Generator().manual_seed(c1 + c2)
+    cl = torch.channels_last
+    fm = (torch.randn(3, c1, h, w, generator=g) * 4).half().to(device).contiguous(memory_format=cl)
+    skip = (torch.randn(3, c2, 2 * h, 2 * w, generator=g) * 4).half().to(device).contiguous(memory_format=cl) \
+        if c2 else None
+    out = upsample2x_cat(fm, skip, cpad)
+    up = torch.nn.UpsamplingBilinear2d(scale_factor=2)(fm)
+    parts = [up] + ([skip] if c2 else [])
+    ref = torch.cat(parts, 1)
+    ref = torch.cat([ref, torch.zeros(3, cpad - ref.shape[1], 2 * h, 2 * w, dtype=ref.dtype, device=device)], 1)
+    assert out.shape == ref.shape and out.is_contiguous(memory_format=cl)
+    d = (out.float() - ref.float()).abs()
+    ulp = torch.clamp(ref.float().abs(), min=2 ** -14) * 2 ** -10
+    assert bool((d <= ulp).all()), float((d / ulp).max())
+    assert torch.equal(out[:, c1:], ref[:, c1:])
+    print(f"exact: {float((d == 0).float().mean()):.4f}")
+
+
+@pytest.mark.gpu
+def test_inference_form_device_fp16_matches_reference(device):
+    """configs[2]'s backbone as the bench runs it (PVNetInference: folded BN,
+    fused upsample + cat, fp16 channels_last) against G4: 1.5e-2 of scale."""
+    net = PVNetInference(_net()).to(device=device, dtype=torch.float16).to(memory_format=torch.channels_last)
+    x = torch.from_numpy(G["x_small"]).to(device).half().contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        seg, ver = net(x)
+    sc = _scale()
+    ds = np.abs(seg.float().cpu().numpy() - G["seg_small"]).max()
+    dv = np.abs(ver.float().cpu().numpy() - G["ver_small"]).max()
+    print(f"inference form fp16 device: max dev {ds:.3e} / {dv:.3e} of scale {sc:.2f}")
+    assert ds <= 1.5e-2 * sc and dv <= 1.5e-2 * sc
