@@ -214,6 +214,9 @@ int pv_uncertainty_pnp_refine(const pv_pnp_batch *batch, const double *init_rt, 
  * out 16-byte aligned.  The blend is ATen's upsample_bilinear2d (align_corners=True) arithmetic in f32. */
 int pv_upsample2x_cat_f16(const void *x, const void *skip, void *out, int32_t n, int32_t hin, int32_t win,
                           int32_t c1, int32_t c2, int32_t cpad, pv_stream_t stream);
+/* the same for f32 maps: c1 and cpad multiples of 4 */
+int pv_upsample2x_cat_f32(const void *x, const void *skip, void *out, int32_t n, int32_t hin, int32_t win,
+                          int32_t c1, int32_t c2, int32_t cpad, pv_stream_t stream);
 
 #ifdef __cplusplus
 }

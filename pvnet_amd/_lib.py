@@ -75,6 +75,7 @@ SIGNATURES = [
     ("pv_uncertainty_pnp_refine", ctypes.c_int,
      [ctypes.POINTER(PnpBatch), c_vp, c_vp, ctypes.POINTER(PnpDiag), c_vp]),
     ("pv_upsample2x_cat_f16", ctypes.c_int, [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp]),
+    ("pv_upsample2x_cat_f32", ctypes.c_int, [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp]),
 ]
 
 _lib = None

@@ -180,33 +180,33 @@ def fold_batchnorm(net: nn.Module) -> nn.Module:
 
 def upsample2x_cat(fm: torch.Tensor, skip: torch.Tensor | None, cpad: int) -> torch.Tensor:
     """``torch.cat([UpsamplingBilinear2d(2)(fm), skip], 1)`` zero-padded to
-    ``cpad`` channels, for channels-last fp16 device tensors, in one HIP pass
-    (``pv_upsample2x_cat_f16``, pvnet_amd/csrc/pvdecoder.hip)."""
+    ``cpad`` channels, for channels-last fp16 / f32 device tensors, in one HIP
+    pass (``pv_upsample2x_cat_f16`` / ``_f32``, pvnet_amd/csrc/pvdecoder.hip)."""
     from pvnet_amd import _lib
     n, c1, h, w = fm.shape
     c2 = 0 if skip is None else skip.shape[1]
     cl = torch.channels_last
-    if fm.dtype != torch.float16 or not fm.is_cuda or not fm.is_contiguous(memory_format=cl):
-        raise RuntimeError("upsample2x_cat: fm must be a channels_last float16 CUDA tensor")
-    if skip is not None and (skip.dtype != torch.float16 or not skip.is_contiguous(memory_format=cl)
+    fn = {torch.float16: "pv_upsample2x_cat_f16", torch.float32: "pv_upsample2x_cat_f32"}.get(fm.dtype)
+    if fn is None or not fm.is_cuda or not fm.is_contiguous(memory_format=cl):
+        raise RuntimeError("upsample2x_cat: fm must be a channels_last float16 / float32 CUDA tensor")
+    if skip is not None and (skip.dtype != fm.dtype or not skip.is_contiguous(memory_format=cl)
                              or tuple(skip.shape) != (n, c2, 2 * h, 2 * w)):
-        raise RuntimeError("upsample2x_cat: skip must be channels_last float16 [n, c2, 2h, 2w]")
-    out = torch.empty((n, cpad, 2 * h, 2 * w), dtype=torch.float16, device=fm.device, memory_format=cl)
+        raise RuntimeError("upsample2x_cat: skip must be channels_last [n, c2, 2h, 2w] of fm's dtype")
+    out = torch.empty((n, cpad, 2 * h, 2 * w), dtype=fm.dtype, device=fm.device, memory_format=cl)
     stream = torch.cuda.current_stream(fm.device).cuda_stream
-    _lib.check(_lib.load().pv_upsample2x_cat_f16(fm.data_ptr(), None if skip is None else skip.data_ptr(),
-                                                 out.data_ptr(), n, h, w, c1, c2, cpad, stream),
-               "pv_upsample2x_cat_f16")
+    _lib.check(getattr(_lib.load(), fn)(fm.data_ptr(), None if skip is None else skip.data_ptr(),
+                                        out.data_ptr(), n, h, w, c1, c2, cpad, stream), fn)
     return out
 
 
 class PVNetInference(nn.Module):
-    """fp16 channels-last inference form of a :class:`PVNet` (configs[2]'s
-    backbone): BatchNorm folded into the convolutions (:func:`fold_batchnorm`),
+    """Channels-last inference form of a :class:`PVNet` (fp16: configs[2]'s
+    backbone; f32: configs[1]'s): BatchNorm folded into the convolutions (:func:`fold_batchnorm`),
     each decoder upsampling fused with the concatenation after it
     (:func:`upsample2x_cat`, one HIP pass instead of two), and the last
     concatenation (32 + 3 channels) zero-padded to 40 channels with ``convraw``'s
     first convolution given 5 zero input channels -- the same function up to
-    rounding (MR:64-79).  Input: a channels_last float16 CUDA batch."""
+    rounding (MR:64-79).  Input: a channels_last float16 / float32 CUDA batch."""
 
     RAW_PAD = 40
 

@@ -150,16 +150,17 @@ def test_inference_form_construction():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
 @pytest.mark.parametrize("c1,c2,cpad,h,w", [(32, 3, 40, 12, 16), (64, 64, 128, 7, 9), (128, 64, 192, 5, 6),
                                             (16, 0, 24, 3, 4)])
-def test_upsample2x_cat_matches_torch(c1, c2, cpad, h, w, device):
+def test_upsample2x_cat_matches_torch(c1, c2, cpad, h, w, dtype, device):
     """The fused HIP decoder step equals ATen's UpsamplingBilinear2d + cat +
-    zero pad on channels_last fp16 (the same f32 blend; at most one fp16 ulp
-    where the two compilers associate or contract differently)."""
+    zero pad on channels_last fp16 / f32 (the same f32 blend; at most one ulp
+    where the two compilers contract differently)."""
     g = torch.Generator().manual_seed(c1 + c2)
     cl = torch.channels_last
-    fm = (torch.randn(3, c1, h, w, generator=g) * 4).half().to(device).contiguous(memory_format=cl)
-    skip = (torch.randn(3, c2, 2 * h, 2 * w, generator=g) * 4).half().to(device).contiguous(memory_format=cl) \
+    fm = (torch.randn(3, c1, h, w, generator=g) * 4).to(device, dtype).contiguous(memory_format=cl)
+    skip = (torch.randn(3, c2, 2 * h, 2 * w, generator=g) * 4).to(device, dtype).contiguous(memory_format=cl) \
         if c2 else None
     out = upsample2x_cat(fm, skip, cpad)
     up = torch.nn.UpsamplingBilinear2d(scale_factor=2)(fm)
@@ -168,7 +169,7 @@ def test_upsample2x_cat_matches_torch(c1, c2, cpad, h, w, device):
     ref = torch.cat([ref, torch.zeros(3, cpad - ref.shape[1], 2 * h, 2 * w, dtype=ref.dtype, device=device)], 1)
     assert out.shape == ref.shape and out.is_contiguous(memory_format=cl)
     d = (out.float() - ref.float()).abs()
-    ulp = torch.clamp(ref.float().abs(), min=2 ** -14) * 2 ** -10
+    ulp = torch.clamp(ref.float().abs(), min=2 ** -14) * (2 ** -10 if dtype == torch.float16 else 2 ** -22)
     assert bool((d <= ulp).all()), float((d / ulp).max())
     assert torch.equal(out[:, c1:], ref[:, c1:])
     print(f"exact: {float((d == 0).float().mean()):.4f}")
@@ -187,3 +188,20 @@ def test_inference_form_device_fp16_matches_reference(device):
     dv = np.abs(ver.float().cpu().numpy() - G["ver_small"]).max()
     print(f"inference form fp16 device: max dev {ds:.3e} / {dv:.3e} of scale {sc:.2f}")
     assert ds <= 1.5e-2 * sc and dv <= 1.5e-2 * sc
+
+
+@pytest.mark.gpu
+def test_inference_form_device_fp32_matches_reference(device):
+    """configs[1]'s backbone in the inference form, f32: 2e-4 of scale, as the
+    plain module on MIOpen."""
+    net = PVNetInference(_net()).to(device=device).to(memory_format=torch.channels_last)
+    with torch.no_grad():
+        seg, ver = net(torch.from_numpy(G["x_small"]).to(device).contiguous(memory_format=torch.channels_last))
+        fx = torch.from_numpy(BI.frame_input()).to(device).contiguous(memory_format=torch.channels_last)
+        fseg, fver = net(fx)
+    sc = _scale()
+    ds = np.abs(seg.cpu().numpy() - G["seg_small"]).max()
+    dv = np.abs(ver.cpu().numpy() - G["ver_small"]).max()
+    print(f"inference form f32 device: max dev {ds:.3e} / {dv:.3e} of scale {sc:.2f}")
+    assert ds <= 2e-4 * sc and dv <= 2e-4 * sc
+    _frame_check(fseg.cpu().numpy(), fver.cpu().numpy(), 2e-4)
