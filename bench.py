@@ -468,13 +468,13 @@ def measure_e2e(dev, half=False, batch=1, iters=30, hn=512, form=None):
     torch.backends.cudnn.benchmark = True      # MIOpen: search the convolution algorithms once
     torch.manual_seed(0)
     dt_ = torch.float16 if half else torch.float32
-    # fp16 batch 32: PVNetInference -- BatchNorm folded into the convolutions
-    # (backbone 16.9 -> 14.5 ms) and each decoder upsampling fused with the
-    # cat after it in one HIP pass (pv_upsample2x_cat_f16); both parity-tested
-    # against G4 (tools/e2e_ab.py: interleaved A/B of the forms).  fp32 batch 1
-    # measured 1.4 % slower folded (the bias pass costs what the BN pass did),
-    # so it runs the plain module.
-    form = form or ("inference" if half else "plain")
+    # PVNetInference: BatchNorm folded into the convolutions and each decoder
+    # upsampling fused with the cat after it in one HIP pass
+    # (pv_upsample2x_cat_f16/_f32), parity-tested against G4.  Interleaved
+    # A/B (tools/e2e_ab.py): fp16 batch 32 plain 1.82k, folded 2.13k,
+    # inference 2.78k images/s; f32 batch 1 plain 488, folded 480, inference
+    # 511 (folding alone does not pay in f32: the bias pass costs the BN pass).
+    form = form or "inference"
     net = PVNet(18, 2).eval()
     if form == "folded":
         net = fold_batchnorm(net)

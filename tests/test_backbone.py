@@ -155,8 +155,9 @@ def test_inference_form_construction():
                                             (16, 0, 24, 3, 4)])
 def test_upsample2x_cat_matches_torch(c1, c2, cpad, h, w, dtype, device):
     """The fused HIP decoder step equals ATen's UpsamplingBilinear2d + cat +
-    zero pad on channels_last fp16 / f32 (the same f32 blend; at most one ulp
-    where the two compilers contract differently)."""
+    zero pad on channels_last fp16 / f32 (the same f32 blend; fp16: at most one
+    ulp; f32: a few roundings of the inputs' size, where the two compilers
+    contract differently)."""
     g = torch.Generator().manual_seed(c1 + c2)
     cl = torch.channels_last
     fm = (torch.randn(3, c1, h, w, generator=g) * 4).to(device, dtype).contiguous(memory_format=cl)
@@ -169,7 +170,10 @@ def test_upsample2x_cat_matches_torch(c1, c2, cpad, h, w, dtype, device):
     ref = torch.cat([ref, torch.zeros(3, cpad - ref.shape[1], 2 * h, 2 * w, dtype=ref.dtype, device=device)], 1)
     assert out.shape == ref.shape and out.is_contiguous(memory_format=cl)
     d = (out.float() - ref.float()).abs()
-    ulp = torch.clamp(ref.float().abs(), min=2 ** -14) * (2 ** -10 if dtype == torch.float16 else 2 ** -22)
+    if dtype == torch.float16:
+        ulp = torch.clamp(ref.float().abs(), min=2 ** -14) * 2 ** -10
+    else:   # f32: a few roundings of terms as large as the inputs (blends may cancel)
+        ulp = torch.full_like(d, 4 * 2 ** -24 * float(fm.abs().max()))
     assert bool((d <= ulp).all()), float((d / ulp).max())
     assert torch.equal(out[:, c1:], ref[:, c1:])
     print(f"exact: {float((d == 0).float().mean()):.4f}")
