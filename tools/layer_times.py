@@ -1,5 +1,5 @@
 """Per-layer device time of the configs[2] backbone (fp16, batch 32,
-channels_last, BN folded): hipEvents around every leaf module and cat /
+channels_last; LT_FORM=inference (default: PVNetInference) or folded): hipEvents around every leaf module and cat /
 upsample in eager mode (after MIOpen's Find has run).  GPU only."""
 import sys
 import collections
@@ -8,11 +8,13 @@ import torch
 from torch import nn
 
 sys.path.insert(0, ".")
-from pvnet_amd.network import PVNet, fold_batchnorm  # noqa: E402
+from pvnet_amd.network import PVNet, PVNetInference, fold_batchnorm  # noqa: E402
 
 torch.backends.cudnn.benchmark = True
 torch.manual_seed(0)
-net = fold_batchnorm(PVNet(18, 2).eval()).cuda().half().to(memory_format=torch.channels_last)
+import os
+net = (PVNetInference(PVNet(18, 2).eval()) if os.environ.get("LT_FORM", "inference") == "inference"
+       else fold_batchnorm(PVNet(18, 2).eval())).cuda().half().to(memory_format=torch.channels_last)
 x = torch.randn(32, 3, 480, 640).cuda().half().contiguous(memory_format=torch.channels_last)
 ev = collections.defaultdict(list)
 pre = {}
