@@ -7,7 +7,8 @@
 // (no 16-byte vector path for the convolution after it).  Exported through
 // include/pvvote.h.
 //
-// Thread = one output pixel x 16 bytes of channels (8 fp16 / 4 f32); the upsampled
+// Thread = one output pixel x 16 bytes of channels (8 fp16 / 4 f32), a block
+// 256 of them along one output row (32-bit index math); the upsampled
 // channels come from four 16-byte loads of the input's neighbours, blended
 // in f32 as ATen's upsample_bilinear2d_nhwc_out_frame does
 // (rheight = (Hin-1)/(Hout-1), src = r * dst, lambdas in f32, the same
@@ -32,13 +33,13 @@ __global__ __launch_bounds__(256) void k_up2_cat(const T *__restrict__ x, const 
     constexpr int V = 16 / sizeof(T);
     typedef typename Vec<T, V>::type vT;
     const int Hout = 2 * Hin, Wout = 2 * Win, cpv = Cpad / V, c1v = C1 / V;
-    const int64_t total = (int64_t)N * Hout * Wout * cpv;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        const int k = (int)(i % cpv);
-        const int64_t pix = i / cpv;                       // n * Hout * Wout + oy * Wout + ox
-        const int ox = (int)(pix % Wout);
-        const int64_t r = pix / Wout;
-        const int oy = (int)(r % Hout), n = (int)(r / Hout);
+    // block (x, y): 256 chunks of output row y (n * Hout + oy); 32-bit index math
+    const int j = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (j >= Wout * cpv) return;
+    const int k = j % cpv, ox = j / cpv;
+    for (int row = (int)blockIdx.y; row < N * Hout; row += (int)gridDim.y) {
+        const int oy = row % Hout, n = row / Hout;
+        const int64_t pix = (int64_t)row * Wout + ox;
         vT v;
         if (k < c1v) {
             const float h1r = rh * (float)oy;
@@ -52,16 +53,16 @@ __global__ __launch_bounds__(256) void k_up2_cat(const T *__restrict__ x, const 
             const vT a = *(const vT *)p, b = *(const vT *)(p + dw), c = *(const vT *)(p + dh),
                      d = *(const vT *)(p + dh + dw);
 #pragma unroll
-            for (int j = 0; j < V; ++j)
-                v[j] = (T)(h0l * (w0l * (float)a[j] + w1l * (float)b[j]) + h1l * (w0l * (float)c[j] + w1l * (float)d[j]));
+            for (int q = 0; q < V; ++q)
+                v[q] = (T)(h0l * (w0l * (float)a[q] + w1l * (float)b[q]) + h1l * (w0l * (float)c[q] + w1l * (float)d[q]));
         } else {
             const int c0 = V * (k - c1v);
-            const T *q = skip + (((int64_t)n * Hout + oy) * Wout + ox) * C2 + c0;
+            const T *q = skip + pix * C2 + c0;
             if (C2 % V == 0 && c0 + V <= C2) {
                 v = *(const vT *)q;
             } else {
 #pragma unroll
-                for (int j = 0; j < V; ++j) v[j] = c0 + j < C2 ? q[j] : (T)0.f;
+                for (int e = 0; e < V; ++e) v[e] = c0 + e < C2 ? q[e] : (T)0.f;
             }
         }
         *(vT *)(out + pix * Cpad + V * k) = v;
@@ -80,9 +81,9 @@ int up2_cat(const void *x, const void *skip, void *out, int32_t n, int32_t hin, 
     const int hout = 2 * hin, wout = 2 * win;
     // ATen's area_pixel_compute_scale with align_corners: (in - 1) / (out - 1) in f32
     const float rh = (float)(hin - 1) / (float)(hout - 1), rw = (float)(win - 1) / (float)(wout - 1);
-    const int64_t total = (int64_t)n * hout * wout * (cpad / V);
-    const int64_t blocks = (total + 255) / 256;
-    const unsigned grid = (unsigned)(blocks < 262144 ? blocks : 262144);
+    if ((int64_t)wout * (cpad / V) >= (1ll << 31) || (int64_t)n * hout >= (1ll << 31)) return PV_EINVAL;
+    const int rows = n * hout;
+    const dim3 grid((unsigned)((wout * (cpad / V) + 255) / 256), (unsigned)(rows < 65535 ? rows : 65535));
     k_up2_cat<T><<<grid, 256, 0, (hipStream_t)stream>>>((const T *)x, (const T *)skip, (T *)out, n, hin, win, c1, c2,
                                                         cpad, rh, rw);
     const hipError_t e = hipGetLastError();
