@@ -2162,7 +2162,11 @@ __global__ __launch_bounds__(256) void k_generate_api(const float *direct, const
 // fast domain take it for their whole row.
 constexpr int kBytePix = 8;
 constexpr int kByteWin = kWave * kBytePix;      // bytes of a row per segment
-constexpr int kByteHB = 64;                      // hypothesis records per batch
+#ifndef PVV_BYTE_HB
+#define PVV_BYTE_HB 64
+#endif
+constexpr int kByteHB = PVV_BYTE_HB;             // hypothesis records per batch (rows per wave, <= 64)
+static_assert(kByteHB <= 64 && kByteHB % 16 == 0, "row masks are 64-bit; quarter blocks take 16 rows");
 constexpr uint32_t kQueuePerWave = 128;          // band pairs a wave queues for its end (LDS)
 
 #ifdef PVVOTE_TRACE_U1
@@ -2349,7 +2353,7 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint
         }
         flagged = __builtin_amdgcn_ballot_w64(lane < nh && rec.w != 0.f);
         __builtin_amdgcn_wave_barrier();
-        recs[lane] = rec;
+        if (lane < kByteHB) recs[lane] = rec;
         __builtin_amdgcn_wave_barrier();
     }
 
@@ -2667,8 +2671,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5, 8))
         const int gq = u % G, rest = u / G;
         v = rest % a.vn;
         w = (rest / a.vn + a.nwin - 1) % a.nwin;
-        h0 = part < 0 ? gq * 256 + q * 64 : gq * 256 + part * 64 + q * 16;
-        nh = part < 0 ? kByteHB : 16;
+        h0 = part < 0 ? gq * 4 * kByteHB + q * kByteHB : gq * 4 * kByteHB + part * kByteHB + q * (kByteHB / 4);
+        nh = part < 0 ? kByteHB : kByteHB / 4;
         wave = uniform(blk * 4 + q);
     } else {
         if (a.xcd) {
@@ -2694,7 +2698,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5, 8))
     v = uniform(v); w = uniform(w); h0 = uniform(h0); nh = uniform(nh);
     float2 hq = make_float2(0.f, 0.f);
     if (lane_id() < nh) hq = *(const float2 *)(a.hypo + ((int64_t)(h0 + lane_id()) * a.vn + v) * 2);
-    hraw[lane_id()] = hq;
+    if (lane_id() < kByteHB) hraw[lane_id()] = hq;
     const float4 *stage = nullptr, *raw = nullptr;
     WinInfo wi{};
     if (WPB == 4 && shared) {
