@@ -208,15 +208,14 @@ class PVNetInference(nn.Module):
     first convolution given 5 zero input channels -- the same function up to
     rounding (MR:64-79).  Input: a channels_last float16 / float32 CUDA batch."""
 
-    RAW_PAD = 40
-
     def __init__(self, net: PVNet):
         super().__init__()
         f = fold_batchnorm(net)
         self.seg_dim = f.seg_dim
         self.resnet18_8s, self.conv8s, self.conv4s, self.conv2s = f.resnet18_8s, f.conv8s, f.conv4s, f.conv2s
         c0 = f.convraw[0]
-        pad = nn.Conv2d(self.RAW_PAD, c0.out_channels, c0.kernel_size, c0.stride, c0.padding, bias=True,
+        self.raw_pad = (c0.in_channels + 7) // 8 * 8          # 35 -> 40 for the reference's dims
+        pad = nn.Conv2d(self.raw_pad, c0.out_channels, c0.kernel_size, c0.stride, c0.padding, bias=True,
                         device=c0.weight.device, dtype=c0.weight.dtype)
         with torch.no_grad():
             pad.weight.zero_()
@@ -230,5 +229,5 @@ class PVNetInference(nn.Module):
         fm = self.conv8s(torch.cat([xfc, x8s], 1))
         fm = self.conv4s(upsample2x_cat(fm, x4s, fm.shape[1] + x4s.shape[1]))
         fm = self.conv2s(upsample2x_cat(fm, x2s, fm.shape[1] + x2s.shape[1]))
-        x = self.convraw(upsample2x_cat(fm, x, self.RAW_PAD))
+        x = self.convraw(upsample2x_cat(fm, x, self.raw_pad))
         return x[:, :self.seg_dim], x[:, self.seg_dim:]
