@@ -688,3 +688,39 @@ def test_workspace_reused_across_shapes(device, rvg):
         run_v3(rvg, md, vd, gd, "", device, keep=keep, max_num=100, _workspace=ws)
         run_v3(rvg, ge["d_mask"], ge["d_vertex"], ge, "d_", device, keep=ge["d_keep"].astype(np.uint8), max_num=300,
                _workspace=ws)
+
+
+def test_random_api_votes_match_oracle(device, rv):
+    """A slice of tools/fuzz_votes.py (which ran 15,448 such cases on the GPU
+    box, profiles/r02_fuzz_votes.txt): random tn / vn / hn / thresholds /
+    coordinate spans with degenerate pixels and hypotheses; dense bytes from
+    both kernels, OR bytes and counts all equal the oracle's."""
+    L = _lib.load()
+    L.pv_debug_set_bytes_mfma.argtypes = [ctypes.c_int32]
+    L.pv_debug_set_bytes_mfma.restype = ctypes.c_int32
+    for case in range(1000, 1024):
+        rng = np.random.default_rng(case)
+        tn, vn = int(rng.integers(1, 3000)), int(rng.integers(1, 4))
+        hn = int(rng.choice([1, 7, 100, 200, 512]))
+        span = float(rng.choice([8.0, 640.0, 5000.0, 50000.0]))
+        thr = float(rng.choice([0.99, 0.9, 0.5, 0.3, 0.999]))
+        coords = (rng.random((tn, 2)) * span).astype(np.float32)
+        ang = rng.uniform(-np.pi, np.pi, (tn, vn))
+        scale = rng.choice([1.0, 1e-7, 0.0, 2e19], size=(tn, vn), p=[0.97, 0.01, 0.01, 0.01])
+        direct = np.stack([np.cos(ang) * scale, np.sin(ang) * scale], -1).astype(np.float32)
+        hyp = (rng.random((hn, vn, 2)) * span * 1.4 - span * 0.2).astype(np.float32)
+        hyp[rng.random((hn, vn)) < 0.03] = 3e7
+        ref = np.zeros((hn, vn, tn), np.uint8)
+        O.voting_for_hypothesis(direct, coords, hyp, ref, thr)
+        dd, cc, hh = cu(direct, device), cu(coords, device), cu(hyp, device)
+        for mfma in (0, 1):
+            prev = L.pv_debug_set_bytes_mfma(mfma)
+            out = torch.zeros(ref.shape, dtype=torch.uint8, device=device)
+            rv.voting_for_hypothesis_dense(dd, cc, hh, out, thr)
+            L.pv_debug_set_bytes_mfma(prev)
+            np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"case {case} mfma={mfma}")
+        init = (rng.random(ref.shape) < 0.1).astype(np.uint8) * 5
+        out = cu(init, device)
+        rv.voting_for_hypothesis(dd, cc, hh, out, thr)
+        np.testing.assert_array_equal(out.cpu().numpy(), np.where(ref == 1, 1, init), err_msg=f"case {case} OR")
+        np.testing.assert_array_equal(rv.vote_counts(dd, cc, hh, thr).cpu().numpy(), ref.sum(2), err_msg=f"case {case}")
