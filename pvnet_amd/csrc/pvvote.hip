@@ -44,7 +44,14 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kCompactChunk = 256;           // pixels per compaction block (one per thread)
 constexpr int kVoteChunk = 256;              // pixels per LDS-staged sub-chunk of the vote waves
-constexpr int kRefineNJ = 32;                // refine blocks per (image, keypoint)
+// refine blocks per (image, keypoint); measured on the 8-in-flight stream
+// (tools/ab_libs.sh, two rounds): 32 -> 42.4-42.8k images/s, 16 -> 43.0-43.1k,
+// 8 -> 43.4-43.7k, 4 -> 37.3-37.5k, 2 -> 33.0-33.2k (fewer blocks hold fewer
+// CU slots while they wait on memory; below 8 a block's serial work shows)
+#ifndef PVV_REFINE_NJ
+#define PVV_REFINE_NJ 8
+#endif
+constexpr int kRefineNJ = PVV_REFINE_NJ;
 // domain of the fast test's error bound
 constexpr float kHypMax = 1.0e17f;           // |hx|,|hy| above -> exact-only hypothesis
 constexpr float kLattice = 2.5e-6f;          // |h - round(h)| below (both axes) -> exact-only
@@ -1672,7 +1679,7 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
     __shared__ double sacc[4][5];
     __shared__ int slast;
     // this block's pixels, loaded before the argmax so both latencies overlap
-    constexpr int U = 4;
+    constexpr int U = 128 / kRefineNJ;    // 32768 pixels per keypoint preloaded
     // (guarded by the buffer's extent P, not by tn: the loads do not wait for
     // tn's; records at t >= tn are read but never used)
     const float4 *eb = pex + ((int64_t)b * vn + v) * P;
@@ -1753,10 +1760,11 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
     }
     __syncthreads();
     if (!slast) return;
-    // ---- last block of image b: each keypoint's kRefineNJ partials (32 consecutive
-    // records = one half-wave) summed by a fixed shuffle tree, and the keypoints'
+    // ---- last block of image b: each keypoint's kRefineNJ partials (consecutive
+    // records = an aligned lane group) summed by a fixed shuffle tree, and the keypoints'
     // winners and ratios, all loads in flight together ----
-    static_assert(kRefineNJ == 32, "a keypoint's partials fill one half-wave");
+    static_assert(kRefineNJ >= 2 && kRefineNJ <= 64 && (kRefineNJ & (kRefineNJ - 1)) == 0,
+                  "a keypoint's partials fill an aligned lane group");
     __shared__ double sks[64][5];
     __shared__ float srat[64];
     __shared__ int swin[64];
@@ -1781,8 +1789,8 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
                 const int i = r0 + r * 256 + (int)threadIdx.x;
 #pragma unroll
                 for (int q = 0; q < 5; ++q)
-                    for (int o = 16; o > 0; o >>= 1) s5[r][q] += __shfl_xor(s5[r][q], o);
-                if ((lane_id() & 31) == 0 && i < nrec)
+                    for (int o = kRefineNJ / 2; o > 0; o >>= 1) s5[r][q] += __shfl_xor(s5[r][q], o);
+                if ((lane_id() & (kRefineNJ - 1)) == 0 && i < nrec)
 #pragma unroll
                     for (int q = 0; q < 5; ++q) sks[i / kRefineNJ][q] = s5[r][q];
             }
