@@ -253,28 +253,51 @@ __device__ __forceinline__ int2 block_sum2(int x, int y, int *sh) {
 }
 
 // ==========================================================================
-// K1: foreground count per 256-pixel block (one pixel per thread) and the
-// block's four wave ballots (k_compact reads 32 B instead of the mask again);
-// zeroes the pipeline's counters
+// K1: foreground count per 256-pixel chunk (one pixel per thread and chunk)
+// and the chunk's four wave ballots (k_compact reads 32 B instead of the mask
+// again); zeroes the pipeline's counters.  A block takes kFgCPB consecutive
+// chunks, their mask loads in flight together (tools/lat_ab.sh, two rounds:
+// 1 chunk 43.8-43.9k images/s and 52.1-52.4 us sequential latency, 2 chunks
+// 43.8k / 52.8-53.1 us, 4 chunks 43.6k / 54.3 us; the former block_sum2 form
+// with two barriers 43.5k / 52.6-52.8 us).
 // ==========================================================================
+#ifndef PVV_FG_CPB
+#define PVV_FG_CPB 1
+#endif
+constexpr int kFgCPB = PVV_FG_CPB;
 template <int KIND, bool EVD>
 __global__ __launch_bounds__(256) void k_fg_count(MaskView m, int H, int W, int32_t *blkcnt, uint64_t *fgbits,
                                                   int nblk, int32_t *zero, int64_t zero_words) {
     static_assert(kCompactChunk == 256, "one pixel per thread");
-    const int b = blockIdx.y, blk = blockIdx.x;
+    const int b = blockIdx.y, wid = threadIdx.x / 64;
     const int64_t P = (int64_t)H * W;
     {   // zero counts + tickets (read only by later kernels of this pipeline)
         int64_t g = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x;
         int64_t G = (int64_t)gridDim.x * gridDim.y * 256;
         for (int64_t i = g; i < zero_words; i += G) zero[i] = 0;
     }
-    __shared__ int sh[8];
-    const int64_t p = (int64_t)blk * kCompactChunk + threadIdx.x;
-    const bool f = p < P && is_fg<KIND, EVD>(m, b, (int)((uint32_t)p / (uint32_t)W), (int)((uint32_t)p % (uint32_t)W));
-    const uint64_t bal = ballot(f);
-    if (lane_id() == 0) fgbits[((int64_t)b * nblk + blk) * 4 + threadIdx.x / 64] = bal;
-    int2 t = block_sum2(f ? 1 : 0, 0, sh);
-    if (threadIdx.x == 0) blkcnt[b * nblk + blk] = t.x;
+    __shared__ int sh[kFgCPB][4];
+    bool f[kFgCPB];
+#pragma unroll
+    for (int k = 0; k < kFgCPB; ++k) {
+        const int blk = blockIdx.x * kFgCPB + k;
+        const int64_t p = (int64_t)blk * kCompactChunk + threadIdx.x;
+        f[k] = blk < nblk && p < P && is_fg<KIND, EVD>(m, b, (int)((uint32_t)p / (uint32_t)W), (int)((uint32_t)p % (uint32_t)W));
+    }
+#pragma unroll
+    for (int k = 0; k < kFgCPB; ++k) {
+        const int blk = blockIdx.x * kFgCPB + k;   // block-uniform
+        if (blk >= nblk) break;
+        const uint64_t bal = ballot(f[k]);
+        if (lane_id() == 0) {
+            fgbits[((int64_t)b * nblk + blk) * 4 + wid] = bal;
+            sh[k][wid] = __popcll(bal);
+        }
+    }
+    __syncthreads();
+    const int blk = blockIdx.x * kFgCPB + (int)threadIdx.x;
+    if (threadIdx.x < kFgCPB && blk < nblk)
+        blkcnt[b * nblk + blk] = sh[threadIdx.x][0] + sh[threadIdx.x][1] + sh[threadIdx.x][2] + sh[threadIdx.x][3];
 }
 
 // foreground total of image b from the per-block counts (every block of K1b/K2 does this)
@@ -3407,7 +3430,7 @@ template <int KIND, bool EVD>
 struct CompactStage {
     static int run(const CompactArgs *a) {
         dim3 grid(a->nblk, a->b);
-        k_fg_count<KIND, EVD><<<grid, 256, 0, a->s>>>(a->m, a->H, a->W, a->ws.blkcnt, a->ws.fgbits, a->nblk, a->ws.counts,
+        k_fg_count<KIND, EVD><<<dim3((a->nblk + kFgCPB - 1) / kFgCPB, a->b), 256, 0, a->s>>>(a->m, a->H, a->W, a->ws.blkcnt, a->ws.fgbits, a->nblk, a->ws.counts,
                                                       a->ws.zero_words);
         if (a->vx.kind == PV_VERTEX_F32)
             k_compact<KIND, EVD, PV_VERTEX_F32><<<grid, 256, 0, a->s>>>(a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.fgbits, a->ws.dsagg,
