@@ -52,6 +52,14 @@ constexpr int kVoteChunk = 256;              // pixels per LDS-staged sub-chunk 
 #define PVV_REFINE_NJ 8
 #endif
 constexpr int kRefineNJ = PVV_REFINE_NJ;
+#ifndef PVV_REFINE_T
+#define PVV_REFINE_T 256
+#endif
+// refine block threads (tools/lat_ab.sh, same threads per keypoint, two rounds:
+// 8 x 256 43.3-43.8k images/s / 51.9 us sequential latency, 16 x 128 43.0k /
+// 53.6-53.9 us, 32 x 64 41.6k / 59.5 us)
+constexpr int kRT = PVV_REFINE_T;
+constexpr int kRW = kRT / 64;                // ... in waves
 // domain of the fast test's error bound
 constexpr float kHypMax = 1.0e17f;           // |hx|,|hy| above -> exact-only hypothesis
 constexpr float kLattice = 2.5e-6f;          // |h - round(h)| below (both axes) -> exact-only
@@ -1690,7 +1698,7 @@ __device__ inline bool lu2_inv(float a00, float a01, float a10, float a11, float
 // ticket add per block; the last block's wave 0 reads them with sc1 loads
 // (MI355X_MICROARCH.md "Valid forms", row 1).
 // ==========================================================================
-__global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, const float2 *hyp, const float4 *pex,
+__global__ __launch_bounds__(kRT) void k_refine_solve(const int32_t *counts, const float2 *hyp, const float4 *pex,
                                                       const int32_t *tn, int64_t P, int vn, int nh,
                                                       float thr, int32_t *win_out, float *ratio_out, double *refpart,
                                                       double *ksum, int32_t *ticket, float confidence, int max_iter,
@@ -1698,15 +1706,15 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
                                                       pv_v3_diag diag) {
     const int j = blockIdx.x, v = blockIdx.y, b = blockIdx.z;
     const int n = tn[b];
-    __shared__ uint64_t skey[4];
-    __shared__ double sacc[4][5];
+    __shared__ uint64_t skey[kRW];
+    __shared__ double sacc[kRW][5];
     __shared__ int slast;
     // this block's pixels, loaded before the argmax so both latencies overlap
-    constexpr int U = 128 / kRefineNJ;    // 32768 pixels per keypoint preloaded
+    constexpr int U = 32768 / (kRefineNJ * kRT);    // 32768 pixels per keypoint preloaded
     // (guarded by the buffer's extent P, not by tn: the loads do not wait for
     // tn's; records at t >= tn are read but never used)
     const float4 *eb = pex + ((int64_t)b * vn + v) * P;
-    const int t0 = j * 256 + threadIdx.x, tstep = kRefineNJ * 256;
+    const int t0 = j * kRT + threadIdx.x, tstep = kRefineNJ * kRT;
     float4 e[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1718,11 +1726,11 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
     constexpr int kRefineLdsHyp = 1024;
     __shared__ float2 shyp[kRefineLdsHyp];
     if (nh <= kRefineLdsHyp)
-        for (int h = threadIdx.x; h < nh; h += 256) shyp[h] = hyp[((int64_t)b * nh + h) * vn + v];
+        for (int h = threadIdx.x; h < nh; h += kRT) shyp[h] = hyp[((int64_t)b * nh + h) * vn + v];
     // argmax over h, first index on ties: key = count << 32 | ~h
     uint64_t key = 0;
     const int32_t *cnt = counts + ((int64_t)b * vn + v) * nh;
-    for (int h = threadIdx.x; h < nh; h += 256) {
+    for (int h = threadIdx.x; h < nh; h += kRT) {
         uint64_t k2 = ((uint64_t)(uint32_t)cnt[h] << 32) | (uint32_t)(0xffffffffu - (uint32_t)h);
         key = k2 > key ? k2 : key;
     }
@@ -1733,7 +1741,7 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
     if (lane_id() == 0) skey[threadIdx.x / 64] = key;
     __syncthreads();
     key = skey[0];
-    for (int q = 1; q < 4; ++q) key = skey[q] > key ? skey[q] : key;
+    for (int q = 1; q < kRW; ++q) key = skey[q] > key ? skey[q] : key;
     const int win = (int)(0xffffffffu - (uint32_t)key);
     const int wcnt = (int)(key >> 32);
     // RV:570-575: ratio = count / tn; best starts at 0 and is replaced only on a strict increase
@@ -1770,7 +1778,12 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
     if (threadIdx.x < 64) {   // wave 0: publish this block's partials, then take a ticket
         const int k = threadIdx.x;
         double *rp = refpart + (((int64_t)b * vn + v) * kRefineNJ + j) * 5;
-        if (k < 5) st_agent(&rp[k], sacc[0][k] + sacc[1][k] + sacc[2][k] + sacc[3][k]);
+        if (k < 5) {
+            double sk = sacc[0][k];
+#pragma unroll
+            for (int q = 1; q < kRW; ++q) sk += sacc[q][k];
+            st_agent(&rp[k], sk);
+        }
         if (j == 0 && k == 0) {
             st_agent(&win_out[b * vn + v], n > 0 ? win : 0);
             st_agent(&ratio_out[b * vn + v], ratio);
@@ -1795,11 +1808,11 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
         const double *rp = refpart + (int64_t)b * vn * kRefineNJ * 5;
         const int nrec = vn * kRefineNJ;
         constexpr int R = 2;                  // rounds in flight together (vn <= 16: all of them)
-        for (int r0 = 0; r0 < nrec; r0 += R * 256) {
+        for (int r0 = 0; r0 < nrec; r0 += R * kRT) {
             double s5[R][5];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const int i = r0 + r * 256 + (int)threadIdx.x;
+                const int i = r0 + r * kRT + (int)threadIdx.x;
 #pragma unroll
                 for (int q = 0; q < 5; ++q) s5[r][q] = i < nrec ? ld_agent(&rp[i * 5 + q]) : 0.0;
             }
@@ -1809,7 +1822,7 @@ __global__ __launch_bounds__(256) void k_refine_solve(const int32_t *counts, con
             }
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const int i = r0 + r * 256 + (int)threadIdx.x;
+                const int i = r0 + r * kRT + (int)threadIdx.x;
 #pragma unroll
                 for (int q = 0; q < 5; ++q)
                     for (int o = kRefineNJ / 2; o > 0; o >>= 1) s5[r][q] += __shfl_xor(s5[r][q], o);
@@ -3753,7 +3766,7 @@ int pv_ransac_voting_v3(const pv_image_desc *img, const pv_vote_params *prm, flo
     if ((r = front_half(img, prm, nh, false, w, dg, s))) return r;
     const int b = img->b, vn = img->vn;
     const int64_t P = (int64_t)img->H * img->W;
-    k_refine_solve<<<dim3(kRefineNJ, vn, b), 256, 0, s>>>(w.counts, w.hyp, w.pex, w.tn, P, vn, nh,
+    k_refine_solve<<<dim3(kRefineNJ, vn, b), kRT, 0, s>>>(w.counts, w.hyp, w.pex, w.tn, P, vn, nh,
                                                           prm->inlier_thresh, w.win, w.ratio, w.refpart, w.ksum,
                                                           w.ticket,
                                                           prm->confidence, prm->max_iter, out, dg);
