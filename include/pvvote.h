@@ -53,6 +53,7 @@ typedef void *pv_stream_t; /* hipStream_t */
 #define PV_VOTE_DENSE 1    /* overwrite every byte with 0/1 (identical for the zero tensors every RV call site passes) */
 
 const char *pv_version(void);
+const char *pv_build_config(void); /* the build's compile-time kernel choices and grid shapes (static string) */
 const char *pv_error_string(int code);
 int pv_device_arch(char *buf, int len); /* writes the gcnArchName of the current device (host pointer) */
 

@@ -53,6 +53,7 @@ class PnpDiag(ctypes.Structure):
 # (name, restype, argtypes) -- one entry per function declared in include/pvvote.h
 SIGNATURES = [
     ("pv_version", ctypes.c_char_p, []),
+    ("pv_build_config", ctypes.c_char_p, []),
     ("pv_error_string", ctypes.c_char_p, [ctypes.c_int]),
     ("pv_device_arch", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
     ("pv_generate_hypothesis", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp]),

@@ -37,7 +37,15 @@
 
 #include "../../include/pvvote.h"
 
-#define PV_VERSION "pvvote 0.1 (gfx950)"
+#define PV_VERSION "pvvote 0.2 (gfx950)"
+
+// Per-wave timestamp traces (tools/vote_trace.py, tools/compact_trace.py)
+// exist only in trace builds (-DPVV_TRACE); the product kernels carry none.
+#ifdef PVV_TRACE
+#define PVV_TRACE_ON(a) ((a).trace != nullptr)
+#else
+#define PVV_TRACE_ON(a) false
+#endif
 
 namespace {
 
@@ -327,11 +335,15 @@ __device__ __forceinline__ int2 image_totals(const int32_t *cnt, int nblk, int u
 // ==========================================================================
 // debug-only phase stamps (s_memrealtime) of the compaction blocks; see
 // pv_debug_compact_trace
+#ifdef PVV_TRACE
 __device__ uint64_t g_ctrace[4096 * 4];
 __device__ int g_ctrace_on;
 __device__ __forceinline__ void cstamp(int blk, int k) {
     if (g_ctrace_on && threadIdx.x == 0 && blk < 4096) g_ctrace[blk * 4 + k] = __builtin_amdgcn_s_memrealtime();
 }
+#else
+__device__ __forceinline__ void cstamp(int, int) {}
+#endif
 
 struct VertexView {
     const void *p;
@@ -425,13 +437,15 @@ __global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int 
         }
         const bool self_all = g_lb_self != 0;
         int pre = 0;
+        // one deadline per thread (not per predecessor): after kLookbackSpin
+        // the thread stops waiting and counts every unseen predecessor itself,
+        // so no thread waits longer than kLookbackSpin in all
+        const uint64_t t_dead = __builtin_amdgcn_s_memrealtime() + kLookbackSpin;
         for (int j = threadIdx.x; j < blk; j += 256) {
             int v = self_all ? 0 : ld_agent(&agg[j]);
-            if (v == 0 && !self_all) {
-                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                while ((v = ld_agent(&agg[j])) == 0 && __builtin_amdgcn_s_memrealtime() - t0 < kLookbackSpin)
+            if (v == 0 && !self_all)
+                while ((v = ld_agent(&agg[j])) == 0 && __builtin_amdgcn_s_memrealtime() < t_dead)
                     __builtin_amdgcn_s_sleep(1);
-            }
             if (v == 0) {   // block j's kept count from its ballots
                 for (int q = 0; q < 4; ++q) {
                     uint64_t w = fgbits[((int64_t)b * nblk + j) * 4 + q];
@@ -526,6 +540,7 @@ struct VoteArgs {
     uint64_t seed;
     int32_t P, raw_v, raw_t, cnt_v, cnt_h, cnt_bs;
     int32_t tn_host, b, vn, nh, hgn, fast;
+    int32_t b0;                 // GEN: batch index of image 0 of this launch (RNG key: the same pairs in any chunking)
     float thr, tau, gzf, gzr;
     uint64_t *trace;            // debug: per-wave (start, end) s_memrealtime stamps, or nullptr
     int32_t rw[4];              // SH, four resident rounds of blocks: work weights per round (0: even)
@@ -576,7 +591,7 @@ __device__ __forceinline__ float2 item_hyp(const VoteArgs &a, int b, int v, int 
                 t0 = min(max(a.idxs[gid * 2], 0), n - 1);
                 t1 = min(max(a.idxs[gid * 2 + 1], 0), n - 1);
             } else {
-                const uint64_t key = (uint64_t)gid;
+                const uint64_t key = (uint64_t)((((int64_t)a.b0 + b) * a.nh + h) * a.vn + v);
                 t0 = rand_index(a.seed, key * 2, n);
                 t1 = rand_index(a.seed, key * 2 + 1, n);
             }
@@ -1035,7 +1050,7 @@ __device__ __forceinline__ void vote_segment(const VoteArgs &a, VoteSlab<PREPPED
             const int nit = (np + 7) >> 3;
 #endif
             F4 a0 = stage[0], a1 = stage[1], a2 = stage[2], a3 = stage[3];
-            if (a.trace && tloop == 0) tloop = __builtin_amdgcn_s_memrealtime();   // (debug traces only)
+            if (PVV_TRACE_ON(a) && tloop == 0) tloop = __builtin_amdgcn_s_memrealtime();   // (debug traces only)
             for (int it = 0; it < nit; ++it) {
                 const int j = it * 8;
                 if ((j & (kWave - 1)) == 0) {
@@ -1173,7 +1188,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         lo += te - ts;
         ++nseg;
     }
-    if (a.trace && lane_id() == 0) {
+    if (PVV_TRACE_ON(a) && lane_id() == 0) {
         uint32_t hw;
         uint32_t xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
@@ -1265,6 +1280,9 @@ __device__ __forceinline__ uint4 form_row(float ax, float ay, float b) {
 #ifndef PVM_WPE
 #define PVM_WPE 3   // 152 VGPRs, no spills (4: 128, spilled across the hot loop): 40.4k -> 41.5k images/s
 #endif
+#define PVM_WPE_STR2(x) #x
+#define PVM_WPE_STR3(x) PVM_WPE_STR2(x)
+#define PVM_WPE_STR PVM_WPE_STR3(PVM_WPE)
 template <bool PREPPED>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PVM_WPE))) void k_vote_mfma(VoteArgs a) {
     const int lane = lane_id();
@@ -1291,8 +1309,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
     int buf = 0, nfix = 0, nseg = 0, nslow = 0, nxo = 0;
     uint64_t tloop = 0, t_total = 0, t_hyp = 0;
     uint64_t c_stage = 0, c_hot = 0, c_fix = 0, c_seg = 0, c_mark = 0;   // debug: shader cycles per phase
-    auto cyc = [&]() -> uint64_t { return a.trace ? __builtin_amdgcn_s_memtime() : 0; };
-    if (a.trace) t_total = __builtin_amdgcn_s_memrealtime();
+    auto cyc = [&]() -> uint64_t { return PVV_TRACE_ON(a) ? __builtin_amdgcn_s_memtime() : 0; };
+    if (PVV_TRACE_ON(a)) t_total = __builtin_amdgcn_s_memrealtime();
     const float tau = a.tau;
     constexpr float kBig = 3.0e38f;
     int b = 0;
@@ -1347,7 +1365,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
         int cnt[kMSet] = {0, 0, 0, 0};
         corr[lane] = 0;
         corr[64 + lane] = 0;
-        if (a.trace && t_hyp == 0) t_hyp = __builtin_amdgcn_s_memrealtime();
+        if (PVV_TRACE_ON(a) && t_hyp == 0) t_hyp = __builtin_amdgcn_s_memrealtime();
         for (int s0 = ts; s0 < te; s0 += kMChunk) {
             {
                 const uint64_t t = cyc();
@@ -1505,7 +1523,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                 // fragment is read one batch ahead, and the band ballots of a
                 // batch are taken together at its end
                 const f32x16 zero = {};
-                if (a.trace && tloop == 0) tloop = __builtin_amdgcn_s_memrealtime();
+                if (PVV_TRACE_ON(a) && tloop == 0) tloop = __builtin_amdgcn_s_memrealtime();
                 { const uint64_t t = cyc(); c_stage += t - c_mark; c_mark = t; }
                 h4f A = afrag(0);
                 f32x16 c0 = __builtin_amdgcn_mfma_f32_32x32x8f16(A, bf[0], zero, 0, 0, 0);
@@ -1647,12 +1665,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
         ++nseg;
         { const uint64_t t = cyc(); c_fix += t - c_mark; c_mark = t; }
     }
-    if (a.trace && lane == 0) {
+    if (PVV_TRACE_ON(a) && lane == 0) {
         const int wave = (int)(blockIdx.x * 4 + wid);
         uint64_t *q = a.trace + 65536 + wave * 4;
         q[0] = c_seg; q[1] = c_stage; q[2] = c_hot; q[3] = c_fix;
     }
-    if (a.trace && lane == 0) {
+    if (PVV_TRACE_ON(a) && lane == 0) {
         const int wave = (int)(blockIdx.x * 4 + wid);
         uint32_t hw, xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
@@ -1711,6 +1729,8 @@ __global__ __launch_bounds__(kRT) void k_refine_solve(const int32_t *counts, con
     __shared__ int slast;
     // this block's pixels, loaded before the argmax so both latencies overlap
     constexpr int U = 32768 / (kRefineNJ * kRT);    // 32768 pixels per keypoint preloaded
+    static_assert(U >= 1, "PVV_REFINE_NJ * PVV_REFINE_T must not exceed 32768 (preload depth)");
+    static_assert(kRT % 64 == 0 && kRT <= 1024, "PVV_REFINE_T: whole waves, at most 1024 threads");
     // (guarded by the buffer's extent P, not by tn: the loads do not wait for
     // tn's; records at t >= tn are read but never used)
     const float4 *eb = pex + ((int64_t)b * vn + v) * P;
@@ -2224,7 +2244,7 @@ struct ByteArgs {
     uint8_t *out;          // [hn][vn][tn]
     int tn, vn, hn, nwin, nhg, fast;
     float thr, tau, gzf, gzr;
-    int dbg;               // profiling ablation (PVVOTE_DEBUG_BYTES), 0 = normal
+    int dbg;               // test hook (pv_debug_set_bytes_mode): 4 = one-entry band queue
     int xcd;               // XCD-contiguous item ranges (grid a multiple of 8)
     // CU-balanced grid (bal_nt > 0): bal_t full blocks, then bal_nt quarter
     // blocks; per XCD bal_tnx / bal_ttx of each (see k_vote_bytes)
@@ -2578,7 +2598,9 @@ __device__ __forceinline__ void vote_bytes_seg(const ByteArgs &a, F4 *recs, uint
     // Exact pass over what is left -- flagged rows, and band rows that found
     // the queue full: the lane's pixels' reference operands are loaded once
     // (one memory round trip), then the reference's sequence decides.
-    if (a.dbg == 3) dmask = 0;   // profiling ablation only
+#ifdef PVVOTE_ABLATE_U1_EXACT
+    dmask = 0;   // profiling ablation only
+#endif
     if (dmask) {
         float2 ec[kBytePix], ed[kBytePix];
 #pragma unroll
@@ -2837,353 +2859,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5, 8))
 #endif
 }
 
-// --------------------------------------------------------------------------
-// voting_for_hypothesis (dense bytes) on the matrix cores: k_vote_bytes_mfma
-// --------------------------------------------------------------------------
-// The pair's two rotated-frame forms X = tau u.(h'-c'), Y = u x (h'-c') are
-// the same [pixels x 3] by [3 x hypotheses] product as in k_vote_mfma (§5a of
-// fp16 hi/lo-split operands, one v_mfma_f32_32x32x8_f16 per 16
-// pixels x 32 hypotheses); the VALU keeps nz = |Y| - X, the inlier bytes (the
-// sign bits of nz gathered by v_perm) and the band minimum.  The MFMA leaves
-// lane (column c, half k) with 8 pixels of hypothesis c; the A rows are staged
-// so that those are pixels 8k .. 8k+7 of the batch, i.e. 8 contiguous bytes
-// of row c.  They go to a per-wave LDS tile of 32 rows x 128 bytes, band
-// pairs are decided there by the reference's sequence, and the tile leaves as
-// row stores of 16 lanes x 8 bytes (the MFMA's own layout, 32 rows x 16 B per
-// store, measured 2.5x slower than contiguous row segments:
-// tools/store_mfma.hip).
-// Block = 4 waves on one (window of 512 pixels, keypoint); wave = kUSets
-// column sets of 32 hypotheses.  The grid exceeds the resident blocks, so the
-// dispatcher balances the CUs (a later block's staging overlaps the others'
-// matrix work).
-// Measured (tools/u1m_var.sh, rocprof on the U1 call): 39.7-40.2 us against
-// the VALU kernel's 31.3 us -- without stores 30.5-32 us against its 26.4:
-// the matrix-core form does not pay here (K = 16 form 42 us, 4 waves per
-// SIMD with 64-byte tiles 39.8 us, 64 hypotheses per wave 41.1 us), so
-// k_vote_bytes stays the default; PVVOTE_BYTES_MFMA=1 selects this one for
-// A/B runs and the tests check both kernels' bytes.
-constexpr int kUB = 16;                        // pixels per MFMA batch
-constexpr int kUWin = 512;                     // pixels per window (block)
-constexpr int kUBat = kUWin / kUB;             // batches per window (32)
-#ifndef PVU_SUBB
-#define PVU_SUBB 8
-#endif
-constexpr int kUSubB = PVU_SUBB;               // batches per tile
-constexpr int kUSubP = kUSubB * kUB;           // pixels per tile (128)
-constexpr int kUTileRS = kUSubP + 8;           // tile row stride, bytes (34 dwords: conflict-free writes)
-constexpr int kUQueue = 256;                   // band pairs queued per wave
-#ifndef PVU_SETS
-#define PVU_SETS 1
-#endif
-constexpr int kUSets = PVU_SETS;               // 32-hypothesis column sets per wave
-
-struct UArgs {
-    const float *direct;   // [tn][vn][2]
-    const float *coords;   // [tn][2]
-    const float *hypo;     // [hn][vn][2]
-    uint8_t *out;          // [hn][vn][tn]
-    int tn, vn, hn, nwin, nhb, items, per;   // per: items per XCD (0: blockIdx order)
-    float thr, tau, gzm, gzr;
-    int fast, dbg;
-};
-
-__device__ uint64_t *g_utrace;   // debug (pv_debug_set_bytes_utrace): per-wave phase stamps of k_vote_bytes_mfma
-
-#ifndef PVU_WPE
-#define PVU_WPE 3
-#endif
-#ifndef PVU_K16
-#define PVU_K16 0
-#endif
-#if PVU_K16
-typedef _Float16 FragU __attribute__((ext_vector_type(8)));
-#define PVU_MFMA __builtin_amdgcn_mfma_f32_32x32x16_f16
-#else
-typedef h4f FragU;
-#define PVU_MFMA __builtin_amdgcn_mfma_f32_32x32x8f16
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVU_WPE, 8))) void k_vote_bytes_mfma(UArgs a) {
-    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    __shared__ uint4 arows[kUBat][2 * kUB];                 // A rows [batch][2 m + form], 16 KiB
-    __shared__ float4 rawp[kUWin];                          // the window's (c, d) as given, 8 KiB
-    __shared__ float2 hyp_all[4][kUSets * 32];              // each wave's hypotheses as given
-    __shared__ alignas(16) uint8_t tile_all[4][32 * kUTileRS];   // each wave's 32 x 128 byte tile
-    __shared__ uint32_t q_all[4][kUQueue];                  // each wave's band pairs
-    __shared__ float4 part[4];
-    __shared__ int part_x[4];
-    const int lane = lane_id();
-    const int wid = (int)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const int col = lane & 31, half = lane >> 5;
-    int item = (int)blockIdx.x;
-    if (a.per) item = (item % 8) * a.per + item / 8;   // an XCD's blocks: neighbouring items (speed only)
-    if (item >= a.items) return;
-    const int hb = item % a.nhb, rest = item / a.nhb;
-    const int v = uniform(rest % a.vn), w = uniform(rest / a.vn);
-    const int t0 = w * kUWin;
-    const int np = uniform(min(kUWin, a.tn - t0));
-    const int hw0 = (hb * 4 + wid) * (kUSets * 32);          // the wave's first hypothesis
-    float2 *hyp = hyp_all[wid];
-    uint8_t *tile = tile_all[wid];
-    uint32_t *bq = q_all[wid];
-    __builtin_amdgcn_s_setprio(3);
-
-    // ---- loads: the window's pixels (2 per thread), the wave's hypotheses ----
-    float2 c[2], d[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int tt = k * 256 + (int)threadIdx.x;
-        c[k] = d[k] = make_float2(0.f, 0.f);
-        if (tt < np) { c[k] = *(const float2 *)(a.coords + (int64_t)(t0 + tt) * 2);
-                       d[k] = *(const float2 *)(a.direct + ((int64_t)(t0 + tt) * a.vn + v) * 2); }
-    }
-#pragma unroll
-    for (int j = 0; j < kUSets; ++j) {
-        const int h = hw0 + j * 32 + col;
-        if (half == 0) {
-            float2 hv = make_float2(0.f, 0.f);
-            if (h < a.hn) hv = *(const float2 *)(a.hypo + ((int64_t)h * a.vn + v) * 2);
-            hyp[j * 32 + col] = hv;
-        }
-    }
-    // ---- the window's frame: bounding-box centre origin, radius, fast domain ----
-    constexpr float kBig = 3.0e38f;
-    float4 q[2];
-    float xl = kBig, xh = -kBig, yl = kBig, yh = -kBig;
-    bool exo = false;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int tt = k * 256 + (int)threadIdx.x;
-        q[k] = make_float4(__builtin_nanf(""), 0.f, 0.f, 0.f);
-        if (tt < np) {
-            // the reference's norm1 gate (KU:119-121); u = n rsq(n.n), rounded
-            // per component (only its direction matters, as in prep_compacted)
-            bool ex;
-            q[k] = prep_compacted(F4{c[k].x, c[k].y, d[k].x, d[k].y}, &ex);
-            exo |= ex;
-            xl = fminf(xl, c[k].x); xh = fmaxf(xh, c[k].x);
-            yl = fminf(yl, c[k].y); yh = fmaxf(yh, c[k].y);
-            rawp[tt] = make_float4(c[k].x, c[k].y, d[k].x, d[k].y);
-        }
-    }
-    xl = wave_min(xl); xh = wave_max(xh);
-    yl = wave_min(yl); yh = wave_max(yh);
-    const bool wexo = __builtin_amdgcn_ballot_w64(exo) != 0;
-    if (lane == 0) { part[wid] = make_float4(xl, xh, yl, yh); part_x[wid] = wexo; }
-    __syncthreads();
-    float cxl = kBig, cxh = -kBig, cyl = kBig, cyh = -kBig;
-    int exq = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const float4 P = part[k];
-        cxl = fminf(cxl, P.x); cxh = fmaxf(cxh, P.y);
-        cyl = fminf(cyl, P.z); cyh = fmaxf(cyh, P.w);
-        exq |= part_x[k];
-    }
-    float ox = floorf(0.5f * cxl + 0.5f * cxh), oy = floorf(0.5f * cyl + 0.5f * cyh);
-    if (!(fabsf(ox) <= 1.6e7f && fabsf(oy) <= 1.6e7f)) { ox = 0.f; oy = 0.f; }
-    const float axr = fmaxf(cxh - ox, ox - cxl), ayr = fmaxf(cyh - oy, oy - cyl);
-    const float R = __builtin_amdgcn_sqrtf(fmaf(axr, axr, ayr * ayr)) * 1.00001f;
-    const float tau = a.tau;
-    // (|b| <= max(tau, 1) R must stay in fp16 range)
-    const bool slow = __builtin_amdgcn_readfirstlane(!a.fast || exq != 0 || !(R * fmaxf(tau, 1.f) <= kMRMax));
-    // ---- A rows: pixel p of batch b at row pair m(p), so that the MFMA hands
-    // lane (column, half k) pixels 8k .. 8k+7 ----
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int tt = k * 256 + (int)threadIdx.x;
-        uint4 rx = make_uint4(0u, 0u, pack_h2((_Float16)0.f, (_Float16)0.f),
-                              pack_h2((_Float16)(-60000.f), (_Float16)0.f));   // never votes: X = -6e4 s
-        uint4 ry = make_uint4(0u, 0u, 0u, 0u);
-        if (q[k].x == q[k].x && !slow) {
-            const float cx = q[k].x - ox, cy = q[k].y - oy;
-            const float axX = tau * q[k].z, ayX = tau * q[k].w;
-            rx = form_row(axX, ayX, fmaf(axX, cx, ayX * cy));
-            ry = form_row(-q[k].w, q[k].z, fmaf(-q[k].w, cx, q[k].z * cy));
-        }
-        const int p = tt & 15, qq = p & 7, m = (qq & 1) + 4 * (qq >> 1) + 2 * (p >> 3);
-        arows[tt >> 4][2 * m] = rx;
-        arows[tt >> 4][2 * m + 1] = ry;
-    }
-    __syncthreads();
-    __builtin_amdgcn_s_setprio(1);
-    const uint64_t t_staged = __builtin_amdgcn_s_memrealtime();
-
-    const float kx = a.gzr / fmaxf(tau, 1e-30f) * 1.0001f, ky = a.gzr * 1.0001f;
-#if PVU_K16
-    // gfx950's K = 16 form: the 8 terms in lane half 0 (k 0..7), zeros in half 1
-    auto afrag = [&](int b) -> FragU {
-        const uint4 r = half ? make_uint4(0u, 0u, 0u, 0u) : arows[b][col];
-        return __builtin_bit_cast(FragU, r);
-    };
-#else
-    const uint2 *arow = (const uint2 *)&arows[0][0];
-    auto afrag = [&](int b) -> FragU { return __builtin_bit_cast(FragU, arow[(b * kUB * 2 + col) * 2 + half]); };
-#endif
-    const f32x16 zero = {};
-    const int64_t rstep = (int64_t)a.vn * a.tn;
-    constexpr uint32_t kSgn01 = 0x0c0c0b09u, kSgn23 = 0x0b090c0cu;   // sign bytes (see vote_bytes_seg)
-    auto pack4 = [](float z0, float z1, float z2, float z3) {
-        const uint32_t p01 = __builtin_amdgcn_perm(__float_as_uint(z1), __float_as_uint(z0), kSgn01);
-        const uint32_t p23 = __builtin_amdgcn_perm(__float_as_uint(z3), __float_as_uint(z2), kSgn23);
-        return (p01 | p23) & 0x01010101u;
-    };
-
-#pragma unroll 1
-    for (int j = 0; j < kUSets; ++j) {
-        const int hc0 = hw0 + j * 32;                   // this set's first hypothesis
-        if (hc0 >= a.hn) break;
-        // ---- B fragment and band of the lane's hypothesis for this frame ----
-        const float2 hv = hyp[j * 32 + col];
-        const int h = hc0 + col;
-        const bool fin = isfinite(hv.x) && isfinite(hv.y);
-        const bool xo = h < a.hn && !slow &&
-                        (!fin || hyp_exact_only(hv.x, hv.y) || !(fabsf(hv.x) < kMHypMax && fabsf(hv.y) < kMHypMax));
-        const bool hf = h < a.hn && !slow && !xo;
-        const uint32_t xcols = (uint32_t)__builtin_amdgcn_ballot_w64(xo && half == 0);
-        FragU bf = {};
-        float gb = -1.f, G = 0.f;
-        {
-            const float hx = hv.x - ox, hy = hv.y - oy;
-            const float mag = fmaxf(fabsf(hx), fabsf(hy));
-            const int e = __builtin_amdgcn_frexp_expf(mag);
-            const int k = hf ? max(0, e - 14) : 0;
-            const float s = __builtin_ldexpf(1.f, -k);
-            const float hxs = hx * s, hys = hy * s;
-            const _Float16 xh_ = (_Float16)hxs, xl_ = (_Float16)(hxs - (float)xh_);
-            const _Float16 yh_ = (_Float16)hys, yl_ = (_Float16)(hys - (float)yh_);
-            const _Float16 sh = (_Float16)s;
-            if (hf) {
-#if PVU_K16
-                if (!half) bf = FragU{xh_, xl_, xh_, yh_, yl_, yh_, sh, sh};
-#else
-                bf = half ? FragU{yl_, yh_, sh, sh} : FragU{xh_, xl_, xh_, yh_};
-#endif
-                const float Bv = (__builtin_amdgcn_sqrtf(fmaf(hx, hx, hy * hy)) * 1.00001f + R) * 1.00001f + 1.f;
-                gb = (a.gzm + a.gzr) * Bv * s * 1.00001f;
-                G = a.gzm * Bv * s * 1.001f;
-            }
-        }
-        // lane's store pointer: row hc0 + kRPS r + srow, bytes 8 sl of a tile row
-        constexpr int kLPR = kUSubP / 8, kRPS = kWave / kLPR;   // lanes per tile row, rows per store
-        const int srow = lane / kLPR, sl = lane % kLPR;
-        uint8_t *sp = a.out + ((int64_t)(hc0 + srow) * a.vn + v) * a.tn + t0 + 8 * sl;
-#pragma unroll 1
-        for (int sc = 0; sc * kUSubP < np; ++sc) {
-            const int pb = sc * kUSubP;                  // the tile's first pixel in the window
-            uint32_t hm = 0;
-            if (!slow) {
-                // ---- hot loop: 8 MFMAs, inlier bytes into the tile, band ballots ----
-                FragU A = afrag(sc * kUSubB);
-                f32x16 cc = PVU_MFMA(A, bf, zero, 0, 0, 0);
-#pragma unroll
-                for (int p = 0; p < kUSubB; ++p) {
-                    f32x16 cn = cc;
-                    if (p + 1 < kUSubB) cn = PVU_MFMA(afrag(sc * kUSubB + p + 1), bf, zero, 0, 0, 0);
-                    float nz[8];
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) nz[r] = fabsf(cc[2 * r + 1]) - cc[2 * r];
-                    const uint32_t lo = pack4(nz[0], nz[1], nz[2], nz[3]);
-                    const uint32_t hi = pack4(nz[4], nz[5], nz[6], nz[7]);
-                    *(uint2 *)(tile + col * kUTileRS + 16 * p + 8 * half) = make_uint2(lo, hi);
-                    float mb = __builtin_elementwise_minimum(__builtin_elementwise_minimum(fabsf(nz[0]), fabsf(nz[1])), fabsf(nz[2]));
-                    mb = __builtin_elementwise_minimum(__builtin_elementwise_minimum(mb, fabsf(nz[3])), fabsf(nz[4]));
-                    mb = __builtin_elementwise_minimum(__builtin_elementwise_minimum(mb, fabsf(nz[5])), fabsf(nz[6]));
-                    mb = __builtin_elementwise_minimum(mb, fabsf(nz[7]));
-                    hm |= __builtin_amdgcn_ballot_w64(mb <= gb) != 0 ? 1u << p : 0u;
-                    cc = cn;
-                }
-                if (a.dbg == 5) hm = 0;   // profiling ablation only (PVVOTE_DEBUG_BYTES=5: wrong bytes)
-                // ---- band: the flagged MFMAs again (bit-identical), each pair
-                // against its own bound (D <= |X|/tau + |Y|, as k_vote_mfma);
-                // inside it the reference's sequence decides the tile byte ----
-                int nq = 0;
-                auto flush = [&]() {
-                    for (int k0 = 0; k0 < nq; k0 += kWave) {
-                        if (k0 + lane < nq) {
-                            const uint32_t en = bq[k0 + lane];
-                            const int pix = (int)(en & 0x1ffu), cl = (int)(en >> 9);
-                            const float4 e = rawp[pix];
-                            const float2 hj = hyp[j * 32 + cl];
-                            tile[cl * kUTileRS + (pix - pb)] = exact_vote(e.z, e.w, e.x, e.y, hj.x, hj.y, a.thr) ? 1 : 0;
-                        }
-                    }
-                    nq = 0;
-                };
-                while (hm) {
-                    const int p = __builtin_ctz(hm);
-                    hm &= hm - 1;
-                    const f32x16 cb = PVU_MFMA(afrag(sc * kUSubB + p), bf, zero, 0, 0, 0);
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) {
-                        const float X = cb[2 * r], Y = cb[2 * r + 1];
-                        const float zq = X - fabsf(Y);
-                        const float g = fmaf(kx, fabsf(X), fmaf(ky, fabsf(Y), G));
-                        const int pix = pb + kUB * p + 8 * half + r;
-                        const bool u = hf && pix < np && fabsf(zq) <= g;
-                        const uint64_t m = __builtin_amdgcn_ballot_w64(u);
-                        if (m) {
-                            if (nq > kUQueue - kWave) flush();
-                            const int at = nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                            if (u) bq[at] = (uint32_t)pix | ((uint32_t)col << 9);
-                            nq += __popcll(m);
-                        }
-                    }
-                }
-                flush();
-            }
-            // ---- exact-only hypotheses (rare), or every pair of a slow window:
-            // lane = pixel, one hypothesis column at a time ----
-            uint32_t xc = slow ? 0xffffffffu : xcols;
-            while (xc) {
-                const int l = __builtin_ctz(xc);
-                xc &= xc - 1;
-                if (hc0 + l >= a.hn) break;
-                const float2 hj = hyp[j * 32 + l];
-#pragma unroll
-                for (int k = 0; k < kUSubP / kWave; ++k) {
-                    const int pl = k * kWave + lane, pix = pb + pl;
-                    bool e = false;
-                    if (pix < np) {
-                        const float4 r = rawp[pix];
-                        e = exact_vote(r.z, r.w, r.x, r.y, hj.x, hj.y, a.thr);
-                    }
-                    tile[l * kUTileRS + pl] = e ? 1 : 0;
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            // ---- the tile's rows: 4 rows x 128 bytes per store ----
-            const bool full = t0 + pb + kUSubP <= a.tn;
-#pragma unroll
-            for (int r = 0; r < 32 / kRPS; ++r) {
-                const int row = kRPS * r + srow;
-                const uint2 x = *(const uint2 *)(tile + row * kUTileRS + 8 * sl);
-                if (hc0 + row < a.hn && a.dbg != 6) {   // (6: profiling ablation, no stores)
-                    uint8_t *p = sp + rstep * (kRPS * r) + pb;
-                    typedef uint64_t u64a1 __attribute__((aligned(1)));
-                    const int t = t0 + pb + 8 * sl;
-                    if (full || t + 8 <= a.tn) {
-                        *(u64a1 *)p = (uint64_t)x.y << 32 | x.x;
-                    } else {
-                        uint64_t y = (uint64_t)x.y << 32 | x.x;
-                        for (int k = 0; k < 8 && t + k < a.tn; ++k) { p[k] = (uint8_t)y; y >>= 8; }
-                    }
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
-    if (g_utrace && lane == 0) {
-        uint64_t *tr = g_utrace + ((int64_t)blockIdx.x * 4 + wid) * 4;
-        uint32_t hw, xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        tr[0] = t_start;
-        tr[1] = t_staged;
-        tr[2] = __builtin_amdgcn_s_memrealtime();
-        tr[3] = ((uint64_t)xcc << 32) | hw;
-    }
-}
-
 // test hook of wave_min / wave_max (pv_debug_wave_minmax)
 __global__ __launch_bounds__(64) void k_debug_minmax(const float *in, float *out) {
     const float x = in[blockIdx.x * 64 + threadIdx.x];
@@ -3311,78 +2986,48 @@ int vote_grid_steps(int64_t pixel_steps, const void *kernel, int max_per_cu = 1 
     return (int)(need < 1 ? 1 : (need < cap ? need : cap));
 }
 
-uint64_t *g_vote_trace = nullptr;   // debug hook (pv_debug_set_vote_trace)
+#ifdef PVV_TRACE
+uint64_t *g_vote_trace = nullptr;   // trace builds only (pv_debug_set_vote_trace)
+#endif
 
-// A/B and debug knobs of pv_voting_for_hypothesis, read from the environment
-// once per process (never per call, so graph captures and eager calls agree)
-struct ByteKnobs {
-    int dbg = 0, wpb = 4, xcd = 1, nobal = 0, mfma = 0;   // mfma: k_vote_bytes_mfma (A/B only)
-};
-ByteKnobs &byte_knobs() {
-    static ByteKnobs k = [] {
-        ByteKnobs r;
-        if (const char *e = getenv("PVVOTE_BYTES_MFMA")) r.mfma = atoi(e);
-        if (const char *e = getenv("PVVOTE_DEBUG_BYTES")) r.dbg = atoi(e);
-        if (const char *e = getenv("PVVOTE_BYTES_WPB")) r.wpb = atoi(e) == 1 ? 1 : 4;
-        if (const char *e = getenv("PVVOTE_BYTES_XCD")) r.xcd = atoi(e);
-        if (const char *e = getenv("PVVOTE_BYTES_NOBAL")) r.nobal = atoi(e);
-        return r;
-    }();
-    return k;
-}
+// Kernel selection and grid shapes are compile-time constants of the build
+// (pvnet_amd/build.py; pv_build_config() reports them): no environment
+// variable changes what the library runs.  The A/B measurements behind each
+// default are in the comments and DESIGN.md section 7.
+#ifndef PVV_VM_BPC
+#define PVV_VM_BPC 3        // k_vote_mfma blocks per CU (tools/vm_ab.sh, 8 in flight: 4 -> 36.6k images/s, 3 -> 40.2k, 2 -> 39.7k)
+#endif
+#ifndef PVV_HYPGEN
+#define PVV_HYPGEN 1        // hypotheses by k_hyp_gen before the vote: 34.6k -> 36.6k images/s, vote 35.2 -> 31.8 us
+#endif
+#ifndef PVV_BYTES_XCD
+#define PVV_BYTES_XCD 1     // k_vote_bytes: XCD-contiguous item ranges (31.1 vs 31.9 us interleaved)
+#endif
+#ifndef PVV_BYTES_BAL
+#define PVV_BYTES_BAL 1     // k_vote_bytes: CU-balanced grid of full + quarter blocks (33.0 -> 31.1 us)
+#endif
+static_assert(PVV_VM_BPC >= 1 && PVV_VM_BPC <= 4, "k_vote_mfma: 1..4 blocks per CU");
 
-// the vote launch: block-shared staging when the groups come in fours
-// (SH: at most 4 of its 5 resident blocks per CU, which measured faster for
-// one launch and leaves room for a concurrent image's small kernels)
-// The VALU vote kernel instead of the matrix-core one: PVVOTE_VC_OLD=1 (A/B
-// runs, read once per process) or pv_debug_set_vote_kernel (the tests run
-// both kernels in one process; set between calls, never during a capture)
-int g_vote_kernel = -1;   // -1: environment / default, 0: k_vote_mfma, 1: k_vote_count
-bool vote_old() {
-    static const bool old = [] { const char *e = getenv("PVVOTE_VC_OLD"); return e && atoi(e) != 0; }();
-    return g_vote_kernel >= 0 ? g_vote_kernel == 1 : old;
-}
-
-// hypotheses by k_hyp_gen before the vote (default; PVVOTE_HYPGEN=0 makes
-// them in the vote kernel's prologue instead, read once per process):
-// measured 34.6k -> 36.6k images/s, vote kernel 35.2 -> 31.8 us (every
-// block of a keypoint otherwise gathers and intersects the same 512 pairs)
-bool hyp_pregen() {
-    static const bool on = [] { const char *e = getenv("PVVOTE_HYPGEN"); return !e || atoi(e) != 0; }();
-    return on;
-}
+// Test hooks (not in pvvote.h, set only by explicit calls between launches,
+// never during a capture): which fused vote/count kernel the pipeline runs
+// (pv_debug_set_vote_kernel: the tests check both in one process) and the
+// byte kernel's band-queue capacity (pv_debug_set_bytes_mode 4: a queue of
+// one entry, so the in-kernel exact pass runs).
+int g_vote_kernel = 0;    // 0: k_vote_mfma (hn a multiple of 512), 1: k_vote_count
+int g_bytes_dbg = 0;
+bool vote_old() { return g_vote_kernel == 1; }
 
 template <bool PREPPED>
 void launch_vote(const VoteArgs &va, int64_t pixel_steps, hipStream_t s) {
     if (va.hgn % 4 == 0 && !vote_old()) {
-        // blocks per CU of the persistent grid (PVVOTE_VM_BPC for A/B, read once)
-        // 3 (measured, tools/vm_ab.sh, 8 images in flight): 4 -> 36.6k images/s,
-        // 3 -> 40.2k, 2 -> 39.7k: with 3 of the 4 wave slots of every SIMD one
-        // launch leaves room for the next image's blocks, whose prologue
-        // (dependent loads) then overlaps this one's matrix/VALU work
-        static const int bpc = [] { const char *e = getenv("PVVOTE_VM_BPC"); const int v = e ? atoi(e) : 3; return v >= 1 && v <= 4 ? v : 3; }();
-        const int grid = vote_grid_steps(pixel_steps, (const void *)k_vote_mfma<PREPPED>, bpc);
+        // blocks per CU of the persistent grid: with 3 of the 4 wave slots
+        // of every SIMD one launch leaves room for the next image's blocks,
+        // whose prologue (dependent loads) then overlaps this one's
+        // matrix/VALU work; the work is cut evenly over the blocks
+        const int grid = vote_grid_steps(pixel_steps, (const void *)k_vote_mfma<PREPPED>, PVV_VM_BPC);
         VoteArgs vr = va;
         vr.gzf = va.fast ? mfma_gz(va.tau) : 0.f;
-        // work weights of the four resident rounds of blocks (round_share;
-        // PVVOTE_VM_RW overrides for A/B runs, read once per process)
-        static const std::array<int, 4> w = [] {
-            // measured (tools/vm_rw.sh, per-SIMD last wave end, p50): even 29.5 us,
-            // 1150/1050/950/850 26.4, 1300/1100/900/700 26.1, 1450/1150/850/550 25.8
-            std::array<int, 4> r{1450, 1150, 850, 550};
-            if (const char *e = getenv("PVVOTE_VM_RW")) sscanf(e, "%d,%d,%d,%d", &r[0], &r[1], &r[2], &r[3]);
-            return r;
-        }();
-        static const std::array<int, 3> w3 = [] {   // the same for three rounds (PVVOTE_VM_RW3)
-            std::array<int, 3> r{0, 0, 0};
-            if (const char *e = getenv("PVVOTE_VM_RW3")) sscanf(e, "%d,%d,%d", &r[0], &r[1], &r[2]);
-            return r;
-        }();
         for (int k = 0; k < 4; ++k) vr.rw[k] = 0;
-        if (grid == 4 * cu_count() && w[0] > 0)
-            for (int k = 0; k < 4; ++k) vr.rw[k] = std::max(w[k], 1);
-        else if (grid == 3 * cu_count() && w3[0] > 0)
-            for (int k = 0; k < 3; ++k) vr.rw[k] = std::max(w3[k], 1);
         k_vote_mfma<PREPPED><<<grid, 256, 0, s>>>(vr);
     } else if (va.hgn % 4 == 0) {
         const int grid = vote_grid_steps(pixel_steps, (const void *)k_vote_count<PREPPED, true>, 4);
@@ -3392,14 +3037,8 @@ void launch_vote(const VoteArgs &va, int64_t pixel_steps, hipStream_t s) {
             // measured: the rounds' mean ends 28.1/30.6/32.9/35.3 us with equal
             // shares, within ~2 us with 1080/1024/976/920, vote kernel -6 %;
             // these a further -1.5 %)
-            // (PVVOTE_VC_RW overrides them for A/B runs; read once per process,
-            // so every launch -- and every graph capture -- sees the same weights)
-            static const std::array<int, 4> w = [] {
-                std::array<int, 4> r{1110, 1035, 965, 890};
-                if (const char *e = getenv("PVVOTE_VC_RW")) sscanf(e, "%d,%d,%d,%d", &r[0], &r[1], &r[2], &r[3]);
-                return r;
-            }();
-            for (int k = 0; k < 4; ++k) vr.rw[k] = w[k] > 0 ? w[k] : 1;
+            constexpr int w[4] = {1110, 1035, 965, 890};
+            for (int k = 0; k < 4; ++k) vr.rw[k] = w[k];
         }
         k_vote_count<PREPPED, true><<<grid, 256, 0, s>>>(vr);
     } else
@@ -3510,12 +3149,14 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
     va.tn_dev = w.tn; va.tn_host = 0;
     va.b = b; va.vn = vn; va.nh = nh; va.hgn = (nh + kGroup - 1) / kGroup;
     fast_constants(prm->inlier_thresh, &va);
+#ifdef PVV_TRACE
     va.trace = g_vote_trace;
+#endif
     // the vote kernel generates the hypotheses itself (item_hyp in its
     // prologue, overlapped with its first pixel loads) and stores them in
     // the reference layout; by default (hyp_pregen) one k_hyp_gen launch makes
     // them first and the vote kernel (k_vote_mfma) reads them keypoint-major
-    if (hyp_pregen() && va.hgn % 4 == 0 && !vote_old()) {
+    if (PVV_HYPGEN && va.hgn % 4 == 0 && !vote_old()) {
         va.hypv_out = w.hypv;
         const int64_t nt = (int64_t)b * nh * vn;
         k_hyp_gen<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(va);
@@ -3535,6 +3176,7 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
         VoteArgs vc = va;
         const int nb = std::min(chunk, b - b0);
         vc.b = nb;
+        vc.b0 = b0;
         vc.pex += (int64_t)b0 * vn * P;
         vc.hyp_out += (int64_t)b0 * nh * vn;
         if (vc.hyp) vc.hyp += (int64_t)b0 * nh * vn;
@@ -3558,6 +3200,20 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
 extern "C" {
 
 const char *pv_version(void) { return PV_VERSION; }
+
+#define PVV_STR2(x) #x
+#define PVV_STR(x) PVV_STR2(x)
+const char *pv_build_config(void) {
+    return "vote=k_vote_mfma(bpc=" PVV_STR(PVV_VM_BPC) ",wpe=" PVM_WPE_STR ",chunk=384)"
+           " hypgen=" PVV_STR(PVV_HYPGEN)
+           " refine=" PVV_STR(PVV_REFINE_NJ) "x" PVV_STR(PVV_REFINE_T)
+           " fg_cpb=" PVV_STR(PVV_FG_CPB)
+           " bytes=k_vote_bytes(rows=" PVV_STR(PVV_BYTE_HB) ",xcd=" PVV_STR(PVV_BYTES_XCD) ",bal=" PVV_STR(PVV_BYTES_BAL) ")"
+#ifdef PVV_TRACE
+           " TRACE"
+#endif
+        ;
+}
 
 const char *pv_error_string(int code) {
     switch (code) {
@@ -3608,42 +3264,20 @@ int pv_voting_for_hypothesis(const float *direct, const float *coords, const flo
     ba.fast = fc.fast; ba.thr = fc.thr; ba.tau = fc.tau; ba.gzf = fc.gzf; ba.gzr = fc.gzr;
     ba.nwin = (tn + kByteWin - 1) / kByteWin;
     ba.nhg = (hn + kByteHB - 1) / kByteHB;
-    const ByteKnobs &kn = byte_knobs();
-    ba.dbg = kn.dbg;
-    if (mode == PV_VOTE_DENSE && kn.mfma) {
-        // the matrix-core kernel (k_vote_bytes_mfma): one block per (window,
-        // keypoint, 4 x kUSets x 32 hypotheses), XCD-grouped item order
-        UArgs ua{};
-        ua.direct = direct; ua.coords = coords; ua.hypo = hypo; ua.out = inliers;
-        ua.tn = tn; ua.vn = vn; ua.hn = hn;
-        ua.nwin = (tn + kUWin - 1) / kUWin;
-        ua.nhb = (hn + 4 * kUSets * 32 - 1) / (4 * kUSets * 32);
-        const int64_t uitems = (int64_t)ua.nwin * vn * ua.nhb;
-        if (uitems >= (1ll << 31) - 8) return PV_EINVAL;
-        ua.items = (int)uitems;
-        ua.per = kn.xcd ? (int)((uitems + 7) / 8) : 0;
-        ua.thr = fc.thr; ua.tau = fc.tau; ua.fast = fc.fast;
-        ua.gzm = fc.fast ? mfma_gz(fc.tau) : 0.f;
-        ua.gzr = fc.gzr;
-        ua.dbg = kn.dbg;
-        const unsigned ugrid = (unsigned)(ua.per ? 8 * (int64_t)ua.per : uitems);
-        k_vote_bytes_mfma<<<ugrid, 256, 0, (hipStream_t)stream>>>(ua);
-        return last();
-    }
+    ba.dbg = g_bytes_dbg;
     const int64_t items = (int64_t)vn * ba.nwin * ba.nhg;
     if (items >= (1ll << 31)) return PV_EINVAL;   // the kernel's 32-bit item index
     // one launch, no scratch: the operands are made where the blocks stage them
-    const int wpb = kn.wpb;                       // waves per block
-    unsigned grid = (unsigned)((items + wpb - 1) / wpb);
-    ba.xcd = kn.xcd;
+    unsigned grid = (unsigned)((items + 3) / 4);
+    ba.xcd = PVV_BYTES_XCD;
     if (ba.xcd) grid = (grid + 7) / 8 * 8;
-    if (wpb == 4 && ba.nhg % 4 == 0 && ba.xcd) {
+    if (PVV_BYTES_BAL && ba.nhg % 4 == 0 && ba.xcd) {
         // CU-balanced grid: full blocks a multiple of the CU count, the rest
         // as quarter blocks, when that leaves at most one quarter block per CU
         // beside four full ones (one resident round; see k_vote_bytes)
         const int64_t units = items / 4, cus = cu_count();
         const int64_t T = units / cus * cus, E = units - T;
-        if (!kn.nobal && T > 0 && T <= 4 * cus && E > 0 && 4 * E <= cus) {
+        if (T > 0 && T <= 4 * cus && E > 0 && 4 * E <= cus) {
             ba.bal_t = (int)T;
             ba.bal_nt = (int)(4 * E);
             ba.bal_tnx = (int)((T + 7) / 8);
@@ -3653,11 +3287,9 @@ int pv_voting_for_hypothesis(const float *direct, const float *coords, const flo
     }
     hipStream_t s = (hipStream_t)stream;
     if (mode == PV_VOTE_DENSE)
-        wpb == 4 ? k_vote_bytes<PV_VOTE_DENSE, 4><<<grid, 256, 0, s>>>(ba)
-                 : k_vote_bytes<PV_VOTE_DENSE, 1><<<grid, 64, 0, s>>>(ba);
+        k_vote_bytes<PV_VOTE_DENSE, 4><<<grid, 256, 0, s>>>(ba);
     else
-        wpb == 4 ? k_vote_bytes<PV_VOTE_OR, 4><<<grid, 256, 0, s>>>(ba)
-                 : k_vote_bytes<PV_VOTE_OR, 1><<<grid, 64, 0, s>>>(ba);
+        k_vote_bytes<PV_VOTE_OR, 4><<<grid, 256, 0, s>>>(ba);
     return last();
 }
 
@@ -3716,36 +3348,33 @@ int pv_debug_lookback_self(int32_t on) {
     return rc(hipMemcpyToSymbol(HIP_SYMBOL(g_lb_self), &on, sizeof(on)));
 }
 
-// debug only (not in pvvote.h): per-wave timestamps of the next pipeline vote launches
+#ifdef PVV_TRACE
+// trace builds only: per-wave timestamps of the next pipeline vote launches
 void pv_debug_set_vote_trace(uint64_t *buf) { g_vote_trace = buf; }
-// debug only (not in pvvote.h): which fused vote/count kernel the pipeline runs
-// (-1 default, 0 matrix-core k_vote_mfma, 1 VALU k_vote_count); returns the previous
+#endif
+// test hook (not in pvvote.h): which fused vote/count kernel the pipeline runs
+// (0 matrix-core k_vote_mfma, 1 VALU k_vote_count); returns the previous
 int pv_debug_set_vote_kernel(int32_t which) {
     const int prev = g_vote_kernel;
-    g_vote_kernel = which < -1 || which > 1 ? -1 : which;
+    g_vote_kernel = which == 1 ? 1 : 0;
     return prev;
 }
-// test hook: the byte kernel's debug mode (PVVOTE_DEBUG_BYTES) at run time; returns the previous one
-// debug: per-wave stamps of k_vote_bytes_mfma into buf (4 x u64 per wave; nullptr: off)
-int pv_debug_set_bytes_utrace(uint64_t *buf) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_utrace), &buf, sizeof(buf)); }
-// test hook: the dense byte kernel (1: k_vote_bytes_mfma, 0: k_vote_bytes); returns the previous
-int pv_debug_set_bytes_mfma(int32_t on) {
-    const int prev = byte_knobs().mfma;
-    byte_knobs().mfma = on;
-    return prev;
-}
+// test hook (not in pvvote.h): the byte kernel's band-queue mode (4: one-entry
+// queue, so band rows take the in-kernel exact pass); returns the previous
 int pv_debug_set_bytes_mode(int32_t dbg) {
-    const int prev = byte_knobs().dbg;
-    byte_knobs().dbg = dbg;
+    const int prev = g_bytes_dbg;
+    g_bytes_dbg = dbg == 4 ? 4 : 0;
     return prev;
 }
 #ifdef PVVOTE_TRACE_U1
 int pv_debug_set_bytes_trace(uint64_t *buf) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_btrace), &buf, sizeof(buf)); }
 #endif
+#ifdef PVV_TRACE
 int pv_debug_compact_trace(int on, uint64_t *host, int n) {
     if (host) return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ctrace), sizeof(uint64_t) * (size_t)n);
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_ctrace_on), &on, sizeof(int));
 }
+#endif
 
 size_t pv_v3_workspace_size(int32_t b, int32_t H, int32_t W, int32_t vn, int32_t n_hyp) {
     if (b <= 0 || H <= 0 || W <= 0 || vn <= 0 || n_hyp <= 0) return 0;

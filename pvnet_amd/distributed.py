@@ -43,14 +43,22 @@ def gather_results(local: torch.Tensor, n_images: int, rank: int, world: int,
     feat = tuple(local.shape[1:])
     if world == 1:
         return local
-    pad = torch.zeros((per,) + feat, dtype=local.dtype, device=local.device)
+    if local.shape[0] != len(range(rank, n_images, world)):
+        raise ValueError(f"rank {rank} holds {local.shape[0]} results, its shard has {len(range(rank, n_images, world))}")
+    # RCCL moves device tensors over xGMI; gloo (the CPU tests, or ranks that
+    # share one device) exchanges host copies -- the collective only, the
+    # results stay where the caller's device put them
+    stage = local.device.type == "cuda" and dist.get_backend(group) == "gloo"
+    dev = torch.device("cpu") if stage else local.device
+    pad = torch.zeros((per,) + feat, dtype=local.dtype, device=dev)
     pad[:local.shape[0]] = local
-    allv = torch.empty((world * per,) + feat, dtype=local.dtype, device=local.device)
+    allv = torch.empty((world * per,) + feat, dtype=local.dtype, device=dev)
     dist.all_gather_into_tensor(allv, pad, group=group)
     allv = allv.view((world, per) + feat)
     # image i = rank i % world, slot i // world
-    idx = torch.arange(n_images, device=local.device)
-    return allv[idx % world, idx // world]
+    idx = torch.arange(n_images, device=dev)
+    out = allv[idx % world, idx // world]
+    return out.to(local.device) if stage else out
 
 
 def run_stream(load: Callable[[int], Sequence[torch.Tensor]], vote: Callable[..., torch.Tensor], n_images: int,

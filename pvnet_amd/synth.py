@@ -50,6 +50,75 @@ def synthetic_field(seed=1234, H=480, W=640, vn=9, radius=97.5, center=(320.0, 2
     return dict(seg=seg, vertex=vertex, mask=m, keypoints=kps, tn=tn)
 
 
+STREAM_KINDS = ("full", "split", "tiny", "large", "corner", "empty", "border", "small")
+
+
+def stream_mask(kind, rng, H=480, W=640):
+    """Foreground of one configs[3] (Occlusion-LINEMOD stream) frame, SURVEY.md
+    8(d)4.  The stream mixes:
+
+    * ``full``   the LINEMOD-cat-sized disk (r 97.5, 29,861 px);
+    * ``split``  an occluded split disk: a disk cut in two by a vertical
+                 occluder band (two pieces, the reference sees one mask);
+    * ``tiny``   a mask below ``min_num`` (< 100 px): the zeros path, RV:537-540;
+    * ``large``  a disk above ``max_num`` (> 30,000 px): Bernoulli
+                 downsampling, RV:543-546;
+    * ``corner`` a disk with one quadrant occluded;
+    * ``empty``  no foreground at all;
+    * ``border`` a disk clipped by the image border;
+    * ``small``  a mask just above ``min_num`` (~100-200 px).
+
+    Centres and sizes are drawn from ``rng`` (numpy Generator)."""
+    yy, xx = np.mgrid[0:H, 0:W]
+
+    def disk(cx, cy, r):
+        return (xx - cx) ** 2 + (yy - cy) ** 2 <= r * r
+
+    cx, cy = rng.uniform(0.3 * W, 0.7 * W), rng.uniform(0.3 * H, 0.7 * H)
+    if kind == "full":
+        return disk(320.0, 240.0, 97.5)
+    if kind == "split":
+        r = rng.uniform(70, 100)
+        band = rng.uniform(0.15, 0.35) * r
+        off = rng.uniform(-0.3, 0.3) * r
+        return disk(cx, cy, r) & ~(np.abs(xx - cx - off) < band)
+    if kind == "tiny":
+        return disk(cx, cy, rng.uniform(2.0, 5.0))
+    if kind == "large":
+        return disk(cx, cy, rng.uniform(105, 130))
+    if kind == "corner":
+        m = disk(cx, cy, rng.uniform(60, 95))
+        return m & ~((xx > cx) & (yy < cy))
+    if kind == "empty":
+        return np.zeros((H, W), bool)
+    if kind == "border":
+        return disk(rng.uniform(-30, 40), rng.uniform(-30, H + 30), rng.uniform(80, 120))
+    if kind == "small":
+        return disk(cx, cy, rng.uniform(6.0, 7.5))
+    raise ValueError(kind)
+
+
+def stream_field(i, seed=9000, H=480, W=640, vn=9, **kw):
+    """Image i of the configs[3] stream: kind ``STREAM_KINDS[i % 8]``
+    (:func:`stream_mask`), field and keypoints as :func:`synthetic_field`
+    with seed ``seed + i``.  Returns synthetic_field's dict plus ``kind``."""
+    kind = STREAM_KINDS[i % len(STREAM_KINDS)]
+    m = stream_mask(kind, np.random.default_rng(seed + 7919 * i), H, W)
+    f = synthetic_field(seed + i, H=H, W=W, vn=vn, mask=m, **kw)
+    f["kind"] = kind
+    return f
+
+
+def keep_mask(fg, max_num, rng):
+    """A downsampling keep-mask for a foreground above ``max_num``: the
+    reference's ``uniform_(0, 1) < max_num / fg`` (RV:543-546), drawn on the
+    host so that a test can inject it into both sides."""
+    fgn = int(np.count_nonzero(fg))
+    if fgn <= max_num:
+        return np.ones(fg.shape, np.uint8)
+    return (rng.random(fg.shape, dtype=np.float32) < np.float32(np.float32(max_num) / np.float32(fgn))).astype(np.uint8)
+
+
 def synthetic_batch(b, seed=1234, **kw):
     """b images S(seed), S(seed+1), ... stacked on dim 0."""
     fs = [synthetic_field(seed + i, **kw) for i in range(b)]

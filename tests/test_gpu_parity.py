@@ -72,21 +72,8 @@ def test_wave_min_max_reduction(device):
 
 
 # ---------------------------------------------------------------- kernels
-@pytest.fixture(params=["mfma", "valu"])
-def bytes_kernel(request):
-    """Both dense byte kernels in one process: the VALU k_vote_bytes (the
-    default) and the matrix-core k_vote_bytes_mfma (A/B option), switched by
-    pv_debug_set_bytes_mfma (a test-only export)."""
-    L = _lib.load()
-    L.pv_debug_set_bytes_mfma.argtypes = [ctypes.c_int32]
-    L.pv_debug_set_bytes_mfma.restype = ctypes.c_int32
-    prev = L.pv_debug_set_bytes_mfma(1 if request.param == "mfma" else 0)
-    yield request.param
-    L.pv_debug_set_bytes_mfma(prev)
-
-
 @pytest.mark.parametrize("case", ["cat_v3_512", "synth_v3_512"])
-def test_generate_and_vote_kernels_bit_exact(case, device, rv, bytes_kernel):
+def test_generate_and_vote_kernels_bit_exact(case, device, rv):
     g = G.load(case)
     mask, vertex = (G.cat_inputs(g) if case.startswith("cat") else G.synth_inputs(g))[:2]
     coords, direct = O.compact(O.fg_mask_v3(mask[0]), vertex[0])
@@ -107,7 +94,7 @@ def test_generate_and_vote_kernels_bit_exact(case, device, rv, bytes_kernel):
         np.testing.assert_array_equal(out.cpu().numpy().sum(2), g["counts"][0][hs])
 
 
-def test_vote_bytes_full_size(device, rv, bytes_kernel):
+def test_vote_bytes_full_size(device, rv):
     """The bench's U1 call (hn=512, tn=29,861: the CU-balanced grid of full
     and quarter blocks): every row's inliers sum to the golden counts, and
     sampled rows -- in full blocks and in quarter blocks -- equal the
@@ -127,7 +114,7 @@ def test_vote_bytes_full_size(device, rv, bytes_kernel):
         np.testing.assert_array_equal(out[torch.from_numpy(rows).to(device)].cpu().numpy(), ref)
 
 
-def test_vote_bytes_balanced_grid_other_shape(device, rv, bytes_kernel):
+def test_vote_bytes_balanced_grid_other_shape(device, rv):
     """hn=256, tn=15,000 (270 units on 256 CUs: 256 full + 56 quarter blocks,
     a different split of the CU-balanced grid): row sums equal the fused
     vote-count kernel's counts, sampled rows equal the oracle's bytes."""
@@ -161,7 +148,7 @@ def test_voting_or_semantics_keeps_existing_bytes(device, rv):
 
 
 @pytest.mark.parametrize("seed", [0, 1, 2])
-def test_guard_band_stress(seed, device, rv, bytes_kernel):
+def test_guard_band_stress(seed, device, rv):
     """Thresholds placed exactly on reference cosines, degenerate pixels and
     hypotheses: every byte must still equal the exact reference decision."""
     rng = np.random.default_rng(seed)
@@ -189,7 +176,7 @@ def test_guard_band_stress(seed, device, rv, bytes_kernel):
 
 
 @pytest.mark.parametrize("span", [5000.0, 40000.0])
-def test_vote_bytes_wide_frames(span, device, rv, bytes_kernel):
+def test_vote_bytes_wide_frames(span, device, rv):
     """API coordinates spread over thousands of pixels at low thresholds: the
     matrix-core kernel's fp16 operands (b = tau u.c' up to tau R) must stay in
     range, or the window takes the exact sequence; fractional coordinates,
@@ -216,7 +203,7 @@ def test_vote_bytes_wide_frames(span, device, rv, bytes_kernel):
 
 
 @pytest.mark.parametrize("full_queue", [False, True])
-def test_band_pairs_both_modes(full_queue, device, rv, bytes_kernel):
+def test_band_pairs_both_modes(full_queue, device, rv):
     """Band pairs go through k_fix_bytes' queue (or, with the queue full, the
     in-kernel exact pass): dense and OR modes, thresholds on reference cosines."""
     L = _lib.load()
@@ -693,11 +680,8 @@ def test_workspace_reused_across_shapes(device, rvg):
 def test_random_api_votes_match_oracle(device, rv):
     """A slice of tools/fuzz_votes.py (which ran 15,448 such cases on the GPU
     box, profiles/r02_fuzz_votes.txt): random tn / vn / hn / thresholds /
-    coordinate spans with degenerate pixels and hypotheses; dense bytes from
-    both kernels, OR bytes and counts all equal the oracle's."""
-    L = _lib.load()
-    L.pv_debug_set_bytes_mfma.argtypes = [ctypes.c_int32]
-    L.pv_debug_set_bytes_mfma.restype = ctypes.c_int32
+    coordinate spans with degenerate pixels and hypotheses; dense bytes, OR
+    bytes and counts all equal the oracle's."""
     for case in range(1000, 1024):
         rng = np.random.default_rng(case)
         tn, vn = int(rng.integers(1, 3000)), int(rng.integers(1, 4))
@@ -713,12 +697,9 @@ def test_random_api_votes_match_oracle(device, rv):
         ref = np.zeros((hn, vn, tn), np.uint8)
         O.voting_for_hypothesis(direct, coords, hyp, ref, thr)
         dd, cc, hh = cu(direct, device), cu(coords, device), cu(hyp, device)
-        for mfma in (0, 1):
-            prev = L.pv_debug_set_bytes_mfma(mfma)
-            out = torch.zeros(ref.shape, dtype=torch.uint8, device=device)
-            rv.voting_for_hypothesis_dense(dd, cc, hh, out, thr)
-            L.pv_debug_set_bytes_mfma(prev)
-            np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"case {case} mfma={mfma}")
+        out = torch.zeros(ref.shape, dtype=torch.uint8, device=device)
+        rv.voting_for_hypothesis_dense(dd, cc, hh, out, thr)
+        np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"case {case} dense")
         init = (rng.random(ref.shape) < 0.1).astype(np.uint8) * 5
         out = cu(init, device)
         rv.voting_for_hypothesis(dd, cc, hh, out, thr)

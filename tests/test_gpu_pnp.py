@@ -195,8 +195,10 @@ def test_ycb21_pose_from_voting(device, eu):
     kp = rvg.ransac_voting_layer_v3(m, v, 512, _idxs=g["v3_idxs"].astype(np.int32))
     _, cov = rvg.estimate_voting_distribution_with_mean(m, v, kp, _idxs=g["evdm_idxs"].astype(np.int32)
                                                         .reshape(1, -1, 21, 2))
+    # device keypoints within 1e-2 px and covariances within 1e-4 (of scale) of the reference's
+    np.testing.assert_allclose(kp.cpu().numpy(), g["v3_keypoints"], atol=1e-2, rtol=0)
+    np.testing.assert_allclose(cov.cpu().numpy(), g["evdm_cov"], rtol=1e-4, atol=1e-4 * np.abs(g["evdm_cov"]).max())
     Rt2 = eu.pose_from_voting(kp, cov, p3, K).cpu().numpy()[0]
-    # device keypoints within 1e-2 px and covariances within 1e-4 of the reference's
     np.testing.assert_allclose(Rt2, ref, atol=1e-4)
 
 
