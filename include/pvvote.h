@@ -219,6 +219,30 @@ int pv_upsample2x_cat_f16(const void *x, const void *skip, void *out, int32_t n,
 int pv_upsample2x_cat_f32(const void *x, const void *skip, void *out, int32_t n, int32_t hin, int32_t win,
                           int32_t c1, int32_t c2, int32_t cpad, pv_stream_t stream);
 
+/* replaces, for channels-last maps, the passes the reference's modules make after each convolution
+ * (lib/networks/resnet.py:41-70 BasicBlock: bn -> relu, bn + residual -> relu; model_repository.py:22-58:
+ * bn -> ReLU / LeakyReLU(0.1); :66-67 the torch.cat after fc), with the BatchNorm folded into a bias:
+ * out[p][0:c1] = act(x[p] + bias (+ (res[p] + rbias))), out[p][c1:c1+c2] = skip[p], in one pass.
+ * x, res: [P][c1]; skip: [P][c2] (NULL when c2 = 0); bias, rbias: [c1] (rbias may be NULL);
+ * out: [P][c1 + c2] (may be x itself when c2 = 0).  act PV_ACT_*; slope for PV_ACT_LEAKY.
+ * fp16: c1, c2 multiples of 8; f32: of 4; all pointers 16-byte aligned.  Roundings as ATen's unfused ops. */
+#define PV_ACT_NONE 0
+#define PV_ACT_RELU 1
+#define PV_ACT_LEAKY 2
+int pv_conv_epilogue_f16(const void *x, const void *bias, const void *res, const void *rbias, const void *skip,
+                         void *out, int64_t P, int32_t c1, int32_t c2, int32_t act, float slope, pv_stream_t stream);
+int pv_conv_epilogue_f32(const void *x, const void *bias, const void *res, const void *rbias, const void *skip,
+                         void *out, int64_t P, int32_t c1, int32_t c2, int32_t act, float slope, pv_stream_t stream);
+
+/* replaces convraw's tail (model_repository.py:53-58 after the 3x3 convolution): BN bias + LeakyReLU(slope)
+ * + the 1x1 convolution to seg_dim + ver_dim channels with its bias, one pass.  x: [P][cin] channels-last
+ * (the 3x3 convolution's output without bias), b1 f32 [cin], w2 f32 [cout][cin], b2 f32 [cout] (device),
+ * out: [P][cout].  (cin, cout) = (32, 20) or (32, 44); x 16-byte, out 8-byte aligned. */
+int pv_head_f16(const void *x, const float *b1, const float *w2, const float *b2, void *out, int64_t P,
+                int32_t cin, int32_t cout, float slope, pv_stream_t stream);
+int pv_head_f32(const void *x, const float *b1, const float *w2, const float *b2, void *out, int64_t P,
+                int32_t cin, int32_t cout, float slope, pv_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

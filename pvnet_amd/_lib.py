@@ -17,6 +17,7 @@ PV_MASK_I64, PV_MASK_U8, PV_MASK_I32, PV_MASK_SEG_F32, PV_MASK_SEG_F16 = 0, 1, 2
 PV_VERTEX_F32, PV_VERTEX_F16 = 0, 1
 PV_VOTE_OR, PV_VOTE_DENSE = 0, 1
 PV_PNP_WEIGHTS, PV_PNP_COV, PV_PNP_COV_V2 = 0, 1, 2
+PV_ACT_NONE, PV_ACT_RELU, PV_ACT_LEAKY = 0, 1, 2
 PNP_STOP = {1: "gradient", 2: "parameter", 3: "function", 4: "max_iterations", 5: "radius", 6: "p3p_only"}
 
 c_i32, c_i64, c_u64, c_f32, c_size, c_vp = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
@@ -75,6 +76,10 @@ SIGNATURES = [
     ("pv_uncertainty_pnp", ctypes.c_int, [ctypes.POINTER(PnpBatch), c_vp, ctypes.POINTER(PnpDiag), c_vp]),
     ("pv_uncertainty_pnp_refine", ctypes.c_int,
      [ctypes.POINTER(PnpBatch), c_vp, c_vp, ctypes.POINTER(PnpDiag), c_vp]),
+    ("pv_conv_epilogue_f16", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_f32, c_vp]),
+    ("pv_conv_epilogue_f32", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_f32, c_vp]),
+    ("pv_head_f16", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_f32, c_vp]),
+    ("pv_head_f32", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_f32, c_vp]),
     ("pv_upsample2x_cat_f16", ctypes.c_int, [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp]),
     ("pv_upsample2x_cat_f32", ctypes.c_int, [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp]),
 ]

@@ -1236,10 +1236,11 @@ __global__ __launch_bounds__(256) void k_hyp_gen(VoteArgs a) {
 // wave64 instruction, min/perm/sad at ~4.3).
 //
 // Exactness: the MFMA path's error is bounded by gzm * |a| * B with
-// B >= |h'| + |c'| (fp16 splits, the f32 sums of the
-// matrix core -- measured within 5.2 ulp of sum|terms| on 2M random
-// 16-term sums, tools/mfma_probe.hip, bounded here by 10 --, the rounded
-// h', c', b and tau u); a pair is decided by the fast sign only if
+// B >= |h'| + |c'| (fp16 splits, the f32 sum of the
+// matrix core's 8 exact products -- bounded by 16 u sum|terms| for any
+// order of roundings (mfma_gz), measured within 5.2 u on 2M random sums
+// (tools/mfma_probe.hip) and tested on crafted cancellation sums --, the
+// rounded h', c', b and tau u); a pair is decided by the fast sign only if
 // |z| > (gzm + gzr) B s (cheap per hypothesis and sub-chunk); the few that
 // are not are re-checked after the sub-chunk against gzm B + gzr D with the
 // pair's own distance D, and decided by the reference's sequence when
@@ -2859,6 +2860,24 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5, 8))
 #endif
 }
 
+// test hook of the matrix-core sums the vote kernel's error bound rests on
+// (pv_debug_mfma_sums): tile i = A [32][8] fp16 x B [8][32] fp16 -> D
+// [32][32] f32 by the instruction k_vote_mfma issues, with a zero accumulator
+// as there; lane l holds A[l & 31][4 (l >> 5) + j] and B[4 (l >> 5) + j][l & 31]
+__global__ __launch_bounds__(64) void k_debug_mfma_sums(const uint16_t *A, const uint16_t *B, float *D) {
+    const int l = threadIdx.x, r = l & 31, h = l >> 5;
+    const uint16_t *At = A + (int64_t)blockIdx.x * 256, *Bt = B + (int64_t)blockIdx.x * 256;
+    h4f a, b;
+    for (int j = 0; j < 4; ++j) {
+        a[j] = __builtin_bit_cast(_Float16, At[r * 8 + 4 * h + j]);
+        b[j] = __builtin_bit_cast(_Float16, Bt[(4 * h + j) * 32 + r]);
+    }
+    const f32x16 zero = {};
+    const f32x16 c = __builtin_amdgcn_mfma_f32_32x32x8f16(a, b, zero, 0, 0, 0);
+    float *Dt = D + (int64_t)blockIdx.x * 1024;
+    for (int i = 0; i < 16; ++i) Dt[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = c[i];
+}
+
 // test hook of wave_min / wave_max (pv_debug_wave_minmax)
 __global__ __launch_bounds__(64) void k_debug_minmax(const float *in, float *out) {
     const float x = in[blockIdx.x * 64 + threadIdx.x];
@@ -2968,11 +2987,16 @@ void fast_constants(float thr, VoteArgs *va) {
 }
 
 // The matrix-core vote (k_vote_mfma): its own fast-path constant (DESIGN.md
-// section 5): per form F the error is <= u |a_F| (31.7 + [X] 2 sqrt 2 tau) B
-// (h', c' and b roundings, fp16 splits 12, b split 4, the matrix core's f32
-// sums 10), z = X - |Y| adds u (tau + 1) B:
-//   gzm = 2 (35.5 tau + 32.7) 2^-24 (2x margin);  gzr as above.
-float mfma_gz(float tau) { return (float)(2.0 * (35.5 * (double)tau + 32.7) / 16777216.0 * 1.0001); }
+// section 5a): per form F the error is <= u |a_F| (37.7 + [X] 2 sqrt 2 tau) B
+// (h', c' and b roundings 5.7, fp16 splits 12, b split 4, the matrix core's
+// f32 sum of 8 exact products 16: any order of its 7 additions, each off by
+// less than one f32 ulp of a partial sum <= sum|terms| -- truncating,
+// k-ordered, or aligned to the largest product and truncated -- stays within
+// 14 u sum|terms|, +1 u for the final rounding, +1 u margin; tested with
+// crafted cancellation sums, test_mfma_sum_error_bound), z = X - |Y| adds
+// u (tau + 1) B:
+//   gzm = 2 (41.5 tau + 38.7) 2^-24 (2x margin);  gzr as above.
+float mfma_gz(float tau) { return (float)(2.0 * (41.5 * (double)tau + 38.7) / 16777216.0 * 1.0001); }
 
 // persistent vote grid: every block resident at once (the occupancy limit of
 // the kernel: LDS slabs, registers), fewer when the work is small (>= ~128
@@ -3336,6 +3360,14 @@ int pv_vote_counts(const float *direct, const float *coords, const float *hypo, 
 }
 
 // debug only (not in pvvote.h): wave min / max of 64 floats per wave -> out[2 * wave + {0, 1}]
+// debug only (not in pvvote.h): ntiles products A[i] (32 x 8 fp16) x B[i] (8 x 32 fp16) -> D[i]
+// (32 x 32 f32) on v_mfma_f32_32x32x8_f16 with a zero accumulator (the vote kernel's sums)
+int pv_debug_mfma_sums(const uint16_t *A, const uint16_t *B, float *D, int32_t ntiles, pv_stream_t stream) {
+    if (!A || !B || !D || ntiles <= 0) return PV_EINVAL;
+    k_debug_mfma_sums<<<(unsigned)ntiles, 64, 0, (hipStream_t)stream>>>(A, B, D);
+    return last();
+}
+
 int pv_debug_wave_minmax(const float *in, float *out, int32_t nwaves, pv_stream_t stream) {
     if (!in || !out || nwaves <= 0) return PV_EINVAL;
     k_debug_minmax<<<(unsigned)nwaves, 64, 0, (hipStream_t)stream>>>(in, out);

@@ -23,6 +23,7 @@ from __future__ import annotations
 import math
 
 import torch
+import torch.nn.functional as F
 from torch import nn
 
 
@@ -199,14 +200,70 @@ def upsample2x_cat(fm: torch.Tensor, skip: torch.Tensor | None, cpad: int) -> to
     return out
 
 
+def _dev_call(fn16, fn32, t: torch.Tensor, *args):
+    from pvnet_amd import _lib
+    fn = {torch.float16: fn16, torch.float32: fn32}.get(t.dtype)
+    if fn is None or not t.is_cuda:
+        raise RuntimeError(f"{fn16[:-4]}: a float16 / float32 CUDA tensor is required")
+    _lib.check(getattr(_lib.load(), fn)(*args, torch.cuda.current_stream(t.device).cuda_stream), fn)
+
+
+_ACT = {"none": 0, "relu": 1, "leaky": 2}
+
+
+def conv_epilogue(y: torch.Tensor, bias: torch.Tensor, act: str = "relu", res: torch.Tensor | None = None,
+                  rbias: torch.Tensor | None = None, skip: torch.Tensor | None = None,
+                  slope: float = 0.1) -> torch.Tensor:
+    """``act(y + bias [+ (res + rbias)])`` over a channels-last conv output in
+    one HIP pass (``pv_conv_epilogue_f16/_f32``), in place -- or, with
+    ``skip``, written beside it as ``torch.cat([.., skip], 1)`` into a new
+    tensor.  ATen's roundings of the unfused bias add / residual add /
+    activation (RN:41-70, MR:22-58)."""
+    n, c1, h, w = y.shape
+    cl = torch.channels_last
+    for t in (y, res, skip):
+        if t is not None and not t.is_contiguous(memory_format=cl):
+            raise RuntimeError("conv_epilogue: channels_last maps required")
+    c2 = 0 if skip is None else skip.shape[1]
+    out = y if skip is None else torch.empty((n, c1 + c2, h, w), dtype=y.dtype, device=y.device, memory_format=cl)
+    _dev_call("pv_conv_epilogue_f16", "pv_conv_epilogue_f32", y, y.data_ptr(), bias.data_ptr(),
+              None if res is None else res.data_ptr(), None if rbias is None else rbias.data_ptr(),
+              None if skip is None else skip.data_ptr(), out.data_ptr(), n * h * w, c1, c2, _ACT[act], float(slope))
+    return out
+
+
+def head(y: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor, slope: float = 0.1) -> torch.Tensor:
+    """convraw's tail (MR:53-58) after its 3x3 convolution: bias + LeakyReLU +
+    the 1x1 convolution with its bias, one HIP pass (``pv_head_f16/_f32``).
+    y [n, 32, h, w] channels_last; b1 / w2 [cout, 32] / b2 float32 device."""
+    n, cin, h, w = y.shape
+    cout = w2.shape[0]
+    if not y.is_contiguous(memory_format=torch.channels_last):
+        raise RuntimeError("head: channels_last input required")
+    out = torch.empty((n, cout, h, w), dtype=y.dtype, device=y.device, memory_format=torch.channels_last)
+    _dev_call("pv_head_f16", "pv_head_f32", y, y.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
+              out.data_ptr(), n * h * w, cin, cout, float(slope))
+    return out
+
+
+def _conv(x, c: nn.Conv2d):
+    """The convolution alone (MIOpen); its folded bias goes to the epilogue."""
+    return F.conv2d(x, c.weight, None, c.stride, c.padding, c.dilation, c.groups)
+
+
 class PVNetInference(nn.Module):
     """Channels-last inference form of a :class:`PVNet` (fp16: configs[2]'s
-    backbone; f32: configs[1]'s): BatchNorm folded into the convolutions (:func:`fold_batchnorm`),
-    each decoder upsampling fused with the concatenation after it
-    (:func:`upsample2x_cat`, one HIP pass instead of two), and the last
-    concatenation (32 + 3 channels) zero-padded to 40 channels with ``convraw``'s
-    first convolution given 5 zero input channels -- the same function up to
-    rounding (MR:64-79).  Input: a channels_last float16 / float32 CUDA batch."""
+    backbone; f32: configs[1]'s): BatchNorm folded into the convolutions
+    (:func:`fold_batchnorm`); after each MIOpen convolution one HIP epilogue
+    pass does the bias, the residual add and the activation
+    (:func:`conv_epilogue`; the ReLU / residual / bias passes of the module
+    form are gone, and fc's epilogue writes the concatenation with x8s
+    itself); each decoder upsampling fused with the concatenation after it
+    (:func:`upsample2x_cat`); the last concatenation (32 + 3 channels)
+    zero-padded to 40 channels with ``convraw``'s first convolution given 5
+    zero input channels; convraw's LeakyReLU and 1x1 convolution one HIP pass
+    (:func:`head`) -- the same function up to rounding (MR:64-79).  Input: a
+    channels_last float16 / float32 CUDA batch."""
 
     def __init__(self, net: PVNet):
         super().__init__()
@@ -224,10 +281,51 @@ class PVNetInference(nn.Module):
         self.convraw = nn.Sequential(pad, *list(f.convraw)[1:])
         self.eval()
 
-    def forward(self, x):
+    def _block(self, blk: BasicBlock, x):
+        y = conv_epilogue(_conv(x, blk.conv1), blk.conv1.bias, "relu")
+        if blk.downsample is None:
+            res, rb = x, None
+        else:
+            res, rb = _conv(x, blk.downsample[0]), blk.downsample[0].bias
+        return conv_epilogue(_conv(y, blk.conv2), blk.conv2.bias, "relu", res=res, rbias=rb)
+
+    def forward_modules(self, x):
+        """The previous inference form (module epilogues: ATen bias / residual /
+        activation passes after each convolution) -- A/B reference only."""
         x2s, x4s, x8s, _, _, xfc = self.resnet18_8s(x)
         fm = self.conv8s(torch.cat([xfc, x8s], 1))
         fm = self.conv4s(upsample2x_cat(fm, x4s, fm.shape[1] + x4s.shape[1]))
         fm = self.conv2s(upsample2x_cat(fm, x2s, fm.shape[1] + x2s.shape[1]))
         x = self.convraw(upsample2x_cat(fm, x, self.raw_pad))
         return x[:, :self.seg_dim], x[:, self.seg_dim:]
+
+    def forward(self, x):
+        r = self.resnet18_8s
+        x2s = conv_epilogue(_conv(x, r.conv1), r.conv1.bias, "relu")
+        y = r.maxpool(x2s)
+        for blk in r.layer1:
+            y = self._block(blk, y)
+        x4s = y
+        for blk in r.layer2:
+            y = self._block(blk, y)
+        x8s = y
+        for layer in (r.layer3, r.layer4):
+            for blk in layer:
+                y = self._block(blk, y)
+        # fc (conv + BN + ReLU, MR:22-26) and torch.cat([xfc, x8s], 1) (MR:66) in one epilogue
+        cat8 = conv_epilogue(_conv(y, r.fc[0]), r.fc[0].bias, "relu", skip=x8s)
+        fm = conv_epilogue(_conv(cat8, self.conv8s[0]), self.conv8s[0].bias, "leaky")
+        fm = upsample2x_cat(fm, x4s, fm.shape[1] + x4s.shape[1])
+        fm = conv_epilogue(_conv(fm, self.conv4s[0]), self.conv4s[0].bias, "leaky")
+        fm = upsample2x_cat(fm, x2s, fm.shape[1] + x2s.shape[1])
+        fm = conv_epilogue(_conv(fm, self.conv2s[0]), self.conv2s[0].bias, "leaky")
+        fm = upsample2x_cat(fm, x, self.raw_pad)
+        c0, c1 = self.convraw[0], self.convraw[3]
+        key = (c0.bias.data_ptr(), c1.weight.data_ptr(), c1.bias.data_ptr(), c1.weight.dtype)
+        if getattr(self, "_head_key", None) != key:     # f32 copies of the head's parameters, made once
+            self._head_w = (c0.bias.detach().float().contiguous(),
+                            c1.weight.detach().float().reshape(c1.out_channels, -1).contiguous(),
+                            c1.bias.detach().float().contiguous())
+            self._head_key = key
+        out = head(_conv(fm, c0), *self._head_w, slope=self.convraw[2].negative_slope)
+        return out[:, :self.seg_dim], out[:, self.seg_dim:]

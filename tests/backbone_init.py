@@ -78,3 +78,26 @@ def frame_summary(seg: np.ndarray, ver: np.ndarray) -> dict:
     return dict(lattice=np.ascontiguousarray(x[:, ::FRAME_STRIDE, ::FRAME_STRIDE]),
                 window=np.ascontiguousarray(x[:, FRAME_WIN[0], FRAME_WIN[1]]),
                 chan_sum=x.astype(np.float64).sum((1, 2)))
+
+
+# The mask fixtures (backbone_g4_masks.npz): the seeded weights with the seg
+# head's foreground logit shifted so that about half of the random frame is
+# foreground -- a mask with long boundaries, i.e. many pixels near the argmax
+# decision -- instead of the ~2 % the plain seeded weights give.
+SEG_BIAS_KEY = "convraw.3.bias"
+
+
+def mask_state_dict(template: dict, shift: float, seed: int = G4_SEED) -> dict:
+    """seeded_state_dict with ``shift`` subtracted from the foreground logit's
+    bias (channel 1 of the last convolution, MR:58 / MR:76)."""
+    sd = seeded_state_dict(template, seed)
+    b = sd[SEG_BIAS_KEY].clone()
+    b[1] = b[1] - np.float32(shift)
+    sd[SEG_BIAS_KEY] = b
+    return sd
+
+
+def fg_bits(seg: np.ndarray) -> np.ndarray:
+    """torch.argmax(seg_pred, 1) == 1 of a [1, 2, H, W] output (first index on
+    ties: class 1 only where l1 > l0), packed (np.packbits, row-major)."""
+    return np.packbits((seg[0, 1] > seg[0, 0]).ravel())

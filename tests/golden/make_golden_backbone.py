@@ -21,7 +21,8 @@ only the .npz this writes).  How the reference is run:
   * Also recorded: how far the reference itself moves in fp16 (CPU half
     convolutions, small input) -- context for the fp16 device tolerance.
 
-Run:  python tests/golden/make_golden_backbone.py  (writes tests/golden/backbone_g4.npz)
+Run:  python tests/golden/make_golden_backbone.py        (writes tests/golden/backbone_g4.npz)
+      python tests/golden/make_golden_backbone.py masks  (writes tests/golden/backbone_g4_masks.npz)
 """
 from __future__ import annotations
 
@@ -97,5 +98,52 @@ def main():
           "fp16 max dev", float(np.abs(h_ver.float().numpy() - s_ver.numpy()).max()))
 
 
+def mask_fixture(mr):
+    """backbone_g4_masks.npz: the reference's full-frame segmentation masks
+    (argmax(seg_pred, 1), tools/demo.py:52, tools/train_linemod.py:254) for
+    PVnet(18, 2) and PVnet(42, 2) (configs[4]'s YCB head, MR:8,57), with the
+    foreground bias shifted so that half the frame is foreground (the shift
+    is computed here from the reference's own output and stored), packed as
+    bits; the pixels whose logit margin |l1 - l0| is below 4e-4 of the output
+    scale (twice the fp32 device tolerance) with their margins; and for
+    PVnet(42, 2) the same small-input outputs / frame summary as G4."""
+    xf = torch.from_numpy(BI.frame_input())
+    xs = torch.from_numpy(BI.small_input())
+    out = {}
+    for vd in (18, 42):
+        ref = mr.PVnet(vd, 2)
+        ref.load_state_dict(BI.seeded_state_dict(ref.state_dict()), strict=True)
+        ref.eval()
+        with torch.no_grad():
+            seg, _ = ref(xf)
+        shift = float(np.float32(np.median((seg[0, 1] - seg[0, 0]).numpy())))
+        sd = BI.mask_state_dict(ref.state_dict(), shift)
+        ref.load_state_dict(sd, strict=True)
+        with torch.no_grad():
+            seg, ver = ref(xf)
+            s_seg, s_ver = ref(xs)
+        seg, ver = seg.numpy(), ver.numpy()
+        d = (seg[0, 1] - seg[0, 0]).ravel()
+        sc = float(np.abs(np.concatenate([seg, ver], 1)).max())
+        low = np.nonzero(np.abs(d) < 4e-4 * sc)[0].astype(np.int32)
+        out.update({f"shift_{vd}": np.float32(shift), f"weights_sha_{vd}": BI.weights_sha(sd),
+                    f"scale_{vd}": np.float64(sc), f"mask_bits_{vd}": BI.fg_bits(seg),
+                    f"fg_count_{vd}": np.int64((d > 0).sum()),
+                    f"margin_idx_{vd}": low, f"margin_val_{vd}": d[low].astype(np.float32)})
+        if vd == 42:
+            out.update(seg_small_42=s_seg.numpy(), ver_small_42=s_ver.numpy())
+            fs = BI.frame_summary(seg, ver)
+            out.update(frame_lattice_42=fs["lattice"], frame_window_42=fs["window"], frame_chan_sum_42=fs["chan_sum"])
+        print(f"PVnet({vd}, 2): shift {shift:.4f}, foreground {int((d > 0).sum())} px, scale {sc:.2f}, "
+              f"{low.size} px within 4e-4 of scale of the decision")
+    out["frame_input_sha"] = BI.sha(BI.frame_input())
+    path = os.path.join(HERE, "backbone_g4_masks.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "masks":
+        mask_fixture(reference_pvnet_module())
+    else:
+        main()
