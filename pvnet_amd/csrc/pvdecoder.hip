@@ -192,9 +192,8 @@ __global__ __launch_bounds__(256) void k_head(const T *__restrict__ x, const flo
     constexpr bool F16 = sizeof(T) == 2;
     constexpr int MT = (COUT + 31) / 32;             // 32-output tiles
     constexpr int KS = F16 ? 4 : 16;                 // MFMA K steps over the 32 channels
-    constexpr int KP = F16 ? 4 : 1;                  // channels per lane and step
     const int lane = (int)(threadIdx.x & 63), m = lane & 31, h = lane >> 5;
-    // channel of (lane half h, step s, j): 16 h + KP s + j
+    // channel of (lane half h, step s, j): 16 h + 4 s + j (fp16), 16 h + s (f32)
     // A fragments (weights): output m + 32 t, the lane's channels
     typedef typename std::conditional<F16, h4, float>::type AF;
     AF wa[MT][KS];
