@@ -1310,6 +1310,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
     int buf = 0, nfix = 0, nseg = 0, nslow = 0, nxo = 0;
     uint64_t tloop = 0, t_total = 0, t_hyp = 0;
     uint64_t c_stage = 0, c_hot = 0, c_fix = 0, c_seg = 0, c_mark = 0;   // debug: shader cycles per phase
+    uint64_t c_band = 0, c_flush = 0, c_xo = 0;                            // (trace builds: parts of c_fix)
     auto cyc = [&]() -> uint64_t { return PVV_TRACE_ON(a) ? __builtin_amdgcn_s_memtime() : 0; };
     if (PVV_TRACE_ON(a)) t_total = __builtin_amdgcn_s_memrealtime();
     const float tau = a.tau;
@@ -1593,25 +1594,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                     const float G = a.gzf * gBj * sj * 1.001f;
                     const f32x16 c = __builtin_amdgcn_mfma_f32_32x32x8f16(afrag(p), bj, zero, 0, 0, 0);
                     // register pair (2q, 2q + 1) = rows 2m, 2m + 1 with
-                    // m = (q & 1) + 4 (q >> 1) + 2 half: pixel m of the batch
+                    // m = (q & 1) + 4 (q >> 1) + 2 half: pixel m of the batch.
+                    // Every pair's test first, one ballot for the lot: most
+                    // flagged MFMAs hold no pair inside its own bound, and
+                    // then the per-pair ballots and queue writes are skipped
+                    uint32_t um = 0;
+                    float zs[8];
 #pragma unroll
                     for (int q = 0; q < 8; ++q) {
                         const float X = c[2 * q], Y = c[2 * q + 1];
                         const float zq = X - fabsf(Y);
                         const float g = fmaf(kx, fabsf(X), fmaf(ky, fabsf(Y), G));
                         const int pix = p * kMB + (q & 1) + 4 * (q >> 1) + 2 * half;
-                        const bool u = fj && pix < np && fabsf(zq) <= g;
-                        const uint64_t m = __builtin_amdgcn_ballot_w64(u);
-                        if (m) {
-                            if (nq > kMQueue - kWave) flush();
-                            const int at = nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                            if (u) bq[at] = (uint32_t)pix | ((uint32_t)j << 9) | ((uint32_t)col << 11) | ((signbit(zq) ? 0u : 1u) << 16);
-                            nq += __popcll(m);
+                        zs[q] = zq;
+                        um |= (fj && pix < np && fabsf(zq) <= g) ? 1u << q : 0u;
+                    }
+                    if (__builtin_amdgcn_ballot_w64(um != 0)) {
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) {
+                            const bool u = (um >> q) & 1u;
+                            const uint64_t m = __builtin_amdgcn_ballot_w64(u);
+                            if (m) {
+                                const int pix = p * kMB + (q & 1) + 4 * (q >> 1) + 2 * half;
+                                if (nq > kMQueue - kWave) flush();
+                                const int at = nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                                if (u) bq[at] = (uint32_t)pix | ((uint32_t)j << 9) | ((uint32_t)col << 11) | ((signbit(zs[q]) ? 0u : 1u) << 16);
+                                nq += __popcll(m);
+                            }
                         }
                     }
                 }
+                { const uint64_t t = cyc(); c_band += t - c_mark; c_fix += t - c_mark; c_mark = t; }
                 flush();
                 __builtin_amdgcn_wave_barrier();
+                { const uint64_t t = cyc(); c_flush += t - c_mark; c_fix += t - c_mark; c_mark = t; }
                 // exact-only hypotheses (rare): lane = pixel, one hypothesis at a time
 #pragma unroll
                 for (int j = 0; j < kMSet; ++j) {
@@ -1638,6 +1654,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                         if (lane == l) cnt[j] += c;
                     }
                 }
+                { const uint64_t t = cyc(); c_xo += t - c_mark; c_fix += t - c_mark; c_mark = t; }
             } else {
                 // every pair through the reference sequence (lane = hypothesis column;
                 // the two lane halves take alternate pixels)
@@ -1668,8 +1685,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
     }
     if (PVV_TRACE_ON(a) && lane == 0) {
         const int wave = (int)(blockIdx.x * 4 + wid);
-        uint64_t *q = a.trace + 65536 + wave * 4;
+        uint64_t *q = a.trace + 65536 + wave * 8;
         q[0] = c_seg; q[1] = c_stage; q[2] = c_hot; q[3] = c_fix;
+        q[4] = c_band; q[5] = c_flush; q[6] = c_xo; q[7] = 0;
     }
     if (PVV_TRACE_ON(a) && lane == 0) {
         const int wave = (int)(blockIdx.x * 4 + wid);
@@ -3031,6 +3049,11 @@ uint64_t *g_vote_trace = nullptr;   // trace builds only (pv_debug_set_vote_trac
 #define PVV_BYTES_BAL 1     // k_vote_bytes: CU-balanced grid of full + quarter blocks (33.0 -> 31.1 us)
 #endif
 static_assert(PVV_VM_BPC >= 1 && PVV_VM_BPC <= 4, "k_vote_mfma: 1..4 blocks per CU");
+#ifndef PVV_VM_RW3_0
+#define PVV_VM_RW3_0 0      // k_vote_mfma work weights of its three dispatch rounds (0: even shares)
+#define PVV_VM_RW3_1 0
+#define PVV_VM_RW3_2 0
+#endif
 
 // Test hooks (not in pvvote.h, set only by explicit calls between launches,
 // never during a capture): which fused vote/count kernel the pipeline runs
@@ -3052,6 +3075,12 @@ void launch_vote(const VoteArgs &va, int64_t pixel_steps, hipStream_t s) {
         VoteArgs vr = va;
         vr.gzf = va.fast ? mfma_gz(va.tau) : 0.f;
         for (int k = 0; k < 4; ++k) vr.rw[k] = 0;
+        // a SIMD issues age-first: with one resident block per CU per dispatch
+        // round, the rounds' waves end in start order (tools/vote_trace.py:
+        // 0 / 3.8 / 7.7 us apart with equal shares); weight the rounds' work
+        if (grid == 3 * cu_count() && PVV_VM_RW3_0 > 0) {
+            vr.rw[0] = PVV_VM_RW3_0; vr.rw[1] = PVV_VM_RW3_1; vr.rw[2] = PVV_VM_RW3_2;
+        }
         k_vote_mfma<PREPPED><<<grid, 256, 0, s>>>(vr);
     } else if (va.hgn % 4 == 0) {
         const int grid = vote_grid_steps(pixel_steps, (const void *)k_vote_count<PREPPED, true>, 4);
@@ -3228,7 +3257,8 @@ const char *pv_version(void) { return PV_VERSION; }
 #define PVV_STR2(x) #x
 #define PVV_STR(x) PVV_STR2(x)
 const char *pv_build_config(void) {
-    return "vote=k_vote_mfma(bpc=" PVV_STR(PVV_VM_BPC) ",wpe=" PVM_WPE_STR ",chunk=384)"
+    return "vote=k_vote_mfma(bpc=" PVV_STR(PVV_VM_BPC) ",wpe=" PVM_WPE_STR ",chunk=384,rw=" PVV_STR(PVV_VM_RW3_0) "/"
+           PVV_STR(PVV_VM_RW3_1) "/" PVV_STR(PVV_VM_RW3_2) ")"
            " hypgen=" PVV_STR(PVV_HYPGEN)
            " refine=" PVV_STR(PVV_REFINE_NJ) "x" PVV_STR(PVV_REFINE_T)
            " fg_cpb=" PVV_STR(PVV_FG_CPB)

@@ -50,21 +50,26 @@ def eager_us(fn, reps=30):
     return float(np.median([x.elapsed_time(y) for x, y in ev])) * 1e3
 
 
-for tn in (29861, 29824, 29696):
-    coords = torch.from_numpy(np.stack([cols[:tn], rows[:tn]], 1).astype(np.float32)).cuda()
-    direct = torch.from_numpy(np.ascontiguousarray(
-        f["vertex"][0].reshape(VN, 2, 480, 640)[:, :, rows[:tn], cols[:tn]].transpose(2, 0, 1))).cuda()
-    idxs = torch.randint(0, tn, (hn, VN, 2), dtype=torch.int32, device="cuda")
-    hyp = rv.generate_hypothesis(direct, coords, idxs)
-    inl = torch.empty((hn, VN, tn), dtype=torch.uint8, device="cuda")
-    vote = lambda: rv.voting_for_hypothesis_dense(direct, coords, hyp, inl, 0.99)  # noqa: E731
-    fill = lambda: inl.fill_(1)  # noqa: E731
-    n = inl.numel()
-    gv, ev_, gf, ef = graph_us(vote), eager_us(vote), graph_us(fill), eager_us(fill)
-    print(f"tn={tn} (mod 128 = {tn % 128}): vote graph {gv:.1f} us ({n / gv / 1e3:.0f} GB/s)  eager {ev_:.1f} us | "
-          f"fill_ graph {gf:.1f} us ({n / gf / 1e3:.0f} GB/s)  eager {ef:.1f} us")
-big = torch.empty(2 * 137_599_488, dtype=torch.uint8, device="cuda")
-for nb in (137_599_488, 2 * 137_599_488):
-    x = big[:nb]
-    g = graph_us(lambda: x.fill_(1))
-    print(f"fill_ {nb / 1e6:.0f} MB graph {g:.1f} us = {nb / g / 1e3:.0f} GB/s")
+def main():
+  for tn in (29861, 29824, 29696):
+      coords = torch.from_numpy(np.stack([cols[:tn], rows[:tn]], 1).astype(np.float32)).cuda()
+      direct = torch.from_numpy(np.ascontiguousarray(
+          f["vertex"][0].reshape(VN, 2, 480, 640)[:, :, rows[:tn], cols[:tn]].transpose(2, 0, 1))).cuda()
+      idxs = torch.randint(0, tn, (hn, VN, 2), dtype=torch.int32, device="cuda")
+      hyp = rv.generate_hypothesis(direct, coords, idxs)
+      inl = torch.empty((hn, VN, tn), dtype=torch.uint8, device="cuda")
+      vote = lambda: rv.voting_for_hypothesis_dense(direct, coords, hyp, inl, 0.99)  # noqa: E731
+      fill = lambda: inl.fill_(1)  # noqa: E731
+      n = inl.numel()
+      gv, ev_, gf, ef = graph_us(vote), eager_us(vote), graph_us(fill), eager_us(fill)
+      print(f"tn={tn} (mod 128 = {tn % 128}): vote graph {gv:.1f} us ({n / gv / 1e3:.0f} GB/s)  eager {ev_:.1f} us | "
+            f"fill_ graph {gf:.1f} us ({n / gf / 1e3:.0f} GB/s)  eager {ef:.1f} us")
+  big = torch.empty(2 * 137_599_488, dtype=torch.uint8, device="cuda")
+  for nb in (137_599_488, 2 * 137_599_488):
+      x = big[:nb]
+      g = graph_us(lambda: x.fill_(1))
+      print(f"fill_ {nb / 1e6:.0f} MB graph {g:.1f} us = {nb / g / 1e3:.0f} GB/s")
+
+
+if __name__ == "__main__":
+    main()

@@ -110,9 +110,14 @@ print("end by block-index quartile (mean):", [f"{k}: {e_us[q == k].mean():.2f}" 
 print("corr(end - SIMD first end, fix steps):", np.corrcoef(erel, nfix)[0, 1])
 # per-phase shader cycles (s_memtime) of each wave: segment setup (hypotheses,
 # first loads), sub-chunk staging, hot loop, band fixes + the rest
-ph = buf.cpu().numpy()[65536:65536 + 4 * 16384].reshape(-1, 4)[:len(t)].astype(np.float64)
+ph = buf.cpu().numpy()[65536:65536 + 8 * 8192].reshape(-1, 8)[:len(t)].astype(np.float64)
 if ph.sum() > 0:
     names = ["seg", "stage", "hot", "fix"]
+    sub = ph[:, 4:7]
+    print("fix parts per wave (median cycles): band re-check %d, exact flush %d, exact-only %d, rest (corrections, "
+          "count atomics) %d" % (np.median(sub[:, 0]), np.median(sub[:, 1]), np.median(sub[:, 2]),
+                                 np.median(ph[:, 3] - sub.sum(1))))
+    ph = ph[:, :4]
     tot = ph.sum(1)
     print("phase cycles per wave (median):", {n: int(np.median(ph[:, k])) for k, n in enumerate(names)},
           "total", int(np.median(tot)))
