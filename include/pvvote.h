@@ -243,6 +243,19 @@ int pv_head_f16(const void *x, const float *b1, const float *w2, const float *b2
 int pv_head_f32(const void *x, const float *b1, const float *w2, const float *b2, void *out, int64_t P,
                 int32_t cin, int32_t cout, float slope, pv_stream_t stream);
 
+/* replaces the decoder's full-resolution tail (model_repository.py:75-79: up2storaw, torch.cat([fm, x], 1),
+ * convraw = 3x3 conv + BN + LeakyReLU(slope) + 1x1 conv) in one fp16 pass on the matrix cores:
+ * fm [n][hin][win][32] (conv2s's output, channels-last), img [n][2hin][2win][3] (the input batch,
+ * channels-last), out [n][2hin][2win][cout], cout = 20 or 44.  w1: [32][368] fp16, the 3x3 weights with
+ * BN folded, k = (3 ky + kx) * 40 + input channel (channels 35..39 and k >= 360 zero); b1 f32 [32];
+ * w2: [cout/32 rounded up][2][32][16] fp16, the 1x1 weights in the accumulator's row order
+ * (element [t][s][m][8h + j] = W[32t + m][(j & 3) + 8 (j >> 2) + 16 s + 4 h], zero past cout); b2 f32
+ * [cout].  fm, w1, w2 16-byte, out 8-byte aligned.  Roundings: the 3x3 sums to fp16 (as a fp16
+ * convolution's output), then ATen's bias add and LeakyReLU, the 1x1 sums to fp16, then its bias add. */
+int pv_decoder_tail_f16(const void *fm, const void *img, const void *w1, const float *b1, const void *w2,
+                        const float *b2, void *out, int32_t n, int32_t hin, int32_t win, int32_t cout, float slope,
+                        pv_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -15,7 +15,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "pvvote.hip")
-SRCS = [SRC, os.path.join(HERE, "csrc", "pvpnp.hip"), os.path.join(HERE, "csrc", "pvdecoder.hip")]
+SRCS = [SRC, os.path.join(HERE, "csrc", "pvpnp.hip"), os.path.join(HERE, "csrc", "pvdecoder.hip"),
+        os.path.join(HERE, "csrc", "pvconv.hip")]
 HDR = os.path.join(REPO, "include", "pvvote.h")
 OUT = os.path.join(HERE, "libpvvote.so")
 ARCH = os.environ.get("PVVOTE_ARCH", "gfx950")

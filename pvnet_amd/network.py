@@ -246,6 +246,52 @@ def head(y: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor, 
     return out
 
 
+def decoder_tail_weights(c0: nn.Conv2d, c1: nn.Conv2d, cin: int = 35):
+    """convraw's weights (MR:53-58, BN folded into ``c0``) laid out for
+    ``pv_decoder_tail_f16`` (include/pvvote.h): w1 [32][368] fp16 with
+    k = (3 ky + kx) * 40 + input channel, b1 f32, w2 in the matrix core
+    accumulator's row order [cout/32][2][32][16] fp16, b2 f32."""
+    co = c0.out_channels
+    if co != 32 or c0.kernel_size != (3, 3) or c1.in_channels != 32 or c1.out_channels not in (20, 44):
+        raise RuntimeError("decoder_tail: convraw must be 3x3 conv to 32 channels and 1x1 conv to 20 / 44")
+    dev = c0.weight.device
+    w = torch.zeros(co, 3, 3, 40, dtype=torch.float32, device=dev)
+    w[..., :cin] = c0.weight.detach().float()[:, :cin].permute(0, 2, 3, 1)
+    w1 = torch.zeros(co, 368, dtype=torch.float32, device=dev)
+    w1[:, :360] = w.reshape(co, 360)
+    cout = c1.out_channels
+    mt = (cout + 31) // 32
+    W2 = torch.zeros(mt * 32, 32, dtype=torch.float32, device=dev)
+    W2[:cout] = c1.weight.detach().float().reshape(cout, 32)
+    s, h, j = torch.meshgrid(torch.arange(2), torch.arange(2), torch.arange(8), indexing="ij")
+    rows = ((j & 3) + 8 * (j >> 2) + 16 * s + 4 * h).to(dev)              # [s][h][j]
+    w2 = W2.reshape(mt, 32, 32)[:, :, rows]                               # [t][m][s][h][j]
+    w2 = w2.permute(0, 2, 1, 3, 4).reshape(mt, 2, 32, 16)
+    return (w1.half().contiguous(), c0.bias.detach().float().contiguous(), w2.half().contiguous(),
+            c1.bias.detach().float().contiguous())
+
+
+def decoder_tail(fm: torch.Tensor, img: torch.Tensor, weights, slope: float = 0.1) -> torch.Tensor:
+    """up2storaw + torch.cat([fm, x], 1) + convraw (MR:75-79) in one fp16
+    matrix-core pass (``pv_decoder_tail_f16``): fm [n, 32, h, w] and img
+    [n, 3, 2h, 2w] channels_last float16 CUDA; ``weights`` from
+    :func:`decoder_tail_weights`.  Returns [n, cout, 2h, 2w] channels_last."""
+    n, c, h, w = fm.shape
+    cl = torch.channels_last
+    if fm.dtype != torch.float16 or img.dtype != torch.float16 or not fm.is_cuda:
+        raise RuntimeError("decoder_tail: float16 CUDA maps required")
+    if c != 32 or tuple(img.shape) != (n, 3, 2 * h, 2 * w):
+        raise RuntimeError("decoder_tail: fm [n, 32, h, w] and img [n, 3, 2h, 2w] required")
+    if not fm.is_contiguous(memory_format=cl) or not img.is_contiguous(memory_format=cl):
+        raise RuntimeError("decoder_tail: channels_last maps required")
+    w1, b1, w2, b2 = weights
+    cout = b2.numel()
+    out = torch.empty((n, cout, 2 * h, 2 * w), dtype=fm.dtype, device=fm.device, memory_format=cl)
+    _dev_call("pv_decoder_tail_f16", None, fm, fm.data_ptr(), img.data_ptr(), w1.data_ptr(), b1.data_ptr(),
+              w2.data_ptr(), b2.data_ptr(), out.data_ptr(), n, h, w, cout, float(slope))
+    return out
+
+
 def _conv(x, c: nn.Conv2d):
     """The convolution alone (MIOpen); its folded bias goes to the epilogue."""
     return F.conv2d(x, c.weight, None, c.stride, c.padding, c.dilation, c.groups)
@@ -279,6 +325,11 @@ class PVNetInference(nn.Module):
             pad.weight[:, :c0.in_channels] = c0.weight
             pad.bias.copy_(c0.bias)
         self.convraw = nn.Sequential(pad, *list(f.convraw)[1:])
+        self.raw_in = c0.in_channels
+        # fp16: convraw's input built and consumed inside one matrix-core kernel (decoder_tail)
+        # when its shapes are the reference's (35 -> 32 -> 20 / 44); False = the MIOpen form
+        self.fused_tail = (c0.in_channels == 35 and c0.out_channels == 32 and f.convraw[3].out_channels in (20, 44)
+                           and self.conv2s[0].out_channels == 32)
         self.eval()
 
     def _block(self, blk: BasicBlock, x):
@@ -319,13 +370,21 @@ class PVNetInference(nn.Module):
         fm = conv_epilogue(_conv(fm, self.conv4s[0]), self.conv4s[0].bias, "leaky")
         fm = upsample2x_cat(fm, x2s, fm.shape[1] + x2s.shape[1])
         fm = conv_epilogue(_conv(fm, self.conv2s[0]), self.conv2s[0].bias, "leaky")
-        fm = upsample2x_cat(fm, x, self.raw_pad)
         c0, c1 = self.convraw[0], self.convraw[3]
+        slope = self.convraw[2].negative_slope
+        if x.dtype == torch.float16 and self.fused_tail:
+            key = (c0.weight.data_ptr(), c0.bias.data_ptr(), c1.weight.data_ptr(), c1.bias.data_ptr())
+            if getattr(self, "_tail_key", None) != key:     # matrix-core layouts of convraw's weights, made once
+                self._tail_w = decoder_tail_weights(c0, c1, self.raw_in)
+                self._tail_key = key
+            out = decoder_tail(fm, x, self._tail_w, slope)
+            return out[:, :self.seg_dim], out[:, self.seg_dim:]
+        fm = upsample2x_cat(fm, x, self.raw_pad)
         key = (c0.bias.data_ptr(), c1.weight.data_ptr(), c1.bias.data_ptr(), c1.weight.dtype)
         if getattr(self, "_head_key", None) != key:     # f32 copies of the head's parameters, made once
             self._head_w = (c0.bias.detach().float().contiguous(),
                             c1.weight.detach().float().reshape(c1.out_channels, -1).contiguous(),
                             c1.bias.detach().float().contiguous())
             self._head_key = key
-        out = head(_conv(fm, c0), *self._head_w, slope=self.convraw[2].negative_slope)
+        out = head(_conv(fm, c0), *self._head_w, slope=slope)
         return out[:, :self.seg_dim], out[:, self.seg_dim:]

@@ -425,3 +425,43 @@ def test_head_matches_torch(cout, dtype, device):
     d = (got.float() - ref.float()).abs().max()
     print(f"head {dtype} cout {cout}: max dev {float(d):.3e} (tolerance {tol:.3e})")
     assert float(d) <= tol
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cout", [20, 44])
+@pytest.mark.parametrize("hw", [(13, 21), (60, 80)])
+def test_decoder_tail_matches_torch(cout, hw, device):
+    """pv_decoder_tail_f16 (up2storaw + cat([fm, x]) + convraw, MR:75-79, one
+    matrix-core pass) against ATen's unfused fp16 ops on the same inputs:
+    F.interpolate + torch.cat + the 3x3 conv + bias + LeakyReLU + the 1x1
+    conv.  Both sum in f32 and round the 3x3 output to fp16 (MIOpen in
+    another order), so the outputs agree within a couple of fp16 roundings
+    of the head's scale; ragged tiles (13 x 21 -> 26 x 42) included."""
+    from pvnet_amd.network import decoder_tail, decoder_tail_weights
+    F = torch.nn.functional
+    g = torch.Generator().manual_seed(cout + hw[0])
+    cl = torch.channels_last
+    n, (h, w) = 2, hw
+    fm = (torch.randn(n, 32, h, w, generator=g) * 2).to(device, torch.float16).contiguous(memory_format=cl)
+    img = torch.randn(n, 3, 2 * h, 2 * w, generator=g).to(device, torch.float16).contiguous(memory_format=cl)
+    c0 = torch.nn.Conv2d(35, 32, 3, 1, 1).to(device)
+    c1 = torch.nn.Conv2d(32, cout, 1).to(device)
+    with torch.no_grad():
+        c0.weight.copy_(torch.randn(32, 35, 3, 3, generator=g) * 0.1)
+        c0.bias.copy_(torch.randn(32, generator=g) * 0.5)
+        c1.weight.copy_(torch.randn(cout, 32, 1, 1, generator=g) * 0.3)
+        c1.bias.copy_(torch.randn(cout, generator=g))
+        c0, c1 = c0.half(), c1.half()
+        up = F.interpolate(fm, scale_factor=2, mode="bilinear", align_corners=True)
+        t = F.leaky_relu(F.conv2d(torch.cat([up, img], 1), c0.weight, None, 1, 1) + c0.bias.view(1, -1, 1, 1), 0.1)
+        ref = c1(t)
+        got = decoder_tail(fm, img, decoder_tail_weights(c0, c1), 0.1)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape and got.is_contiguous(memory_format=cl)
+    sc = float(t.abs().max()) * float(c1.weight.float().abs().sum((1, 2, 3)).max())
+    tol = 2 ** -9 * sc
+    d = (got.float() - ref.float()).abs()
+    print(f"decoder tail cout {cout} {2 * h}x{2 * w}: max dev {float(d.max()):.3e}, "
+          f"mean {float(d.mean()):.3e} (tolerance {tol:.3e}, scale {sc:.2f})")
+    assert float(d.max()) <= tol
+    assert float(d.mean()) <= 2 ** -12 * sc

@@ -1,7 +1,8 @@
 """A/B of the configs[2] backbone (fp16, batch 32, channels_last): the fused
 inference form (PVNetInference.forward) against the module-epilogue form
 (forward_modules), each captured in a hipGraph, interleaved rounds.
-    python tools/backbone_ab.py [rounds] [which: both|fused|modules]"""
+    python tools/backbone_ab.py [rounds] [which: both|fused|tail|modules] [batch]
+(mio_tail: the fused form with convraw on MIOpen + pv_head instead of pv_decoder_tail)"""
 import os
 import sys
 import time
@@ -35,9 +36,19 @@ def graph(fn):
     return g
 
 
+def forward_miopen_tail(x):
+    net.fused_tail = False
+    try:
+        return net.forward(x)
+    finally:
+        net.fused_tail = True
+
+
 gs = {}
 if which in ("both", "fused"):
     gs["fused"] = graph(net.forward)
+if which in ("both", "tail"):
+    gs["mio_tail"] = graph(forward_miopen_tail)
 if which in ("both", "modules"):
     gs["modules"] = graph(net.forward_modules)
 for r in range(rounds):
