@@ -552,6 +552,8 @@ def measure_e2e(dev, half=False, batch=1, iters=30, hn=512, form=None):
     # A/B (tools/e2e_ab.py): fp16 batch 32 plain 1.82k, folded 2.13k,
     # inference 2.78k images/s; f32 batch 1 plain 488, folded 480, inference
     # 511 (folding alone does not pay in f32: the bias pass costs the BN pass).
+    # Backbone alone, fp16 batch 32 (tools/backbone_ab.py, profiles/r03_backbone_ab.txt):
+    # module epilogues 10.4 ms, fused epilogues 8.8 ms, + fused decoder tail 8.2 ms.
     form = form or "inference"
     net = PVNet(18, 2).eval()
     if form == "folded":
@@ -608,8 +610,9 @@ def measure_e2e(dev, half=False, batch=1, iters=30, hn=512, form=None):
                 note="random-init weights (none ship with the reference): timing only; images/s covers backbone + "
                      "v3 in one graph; backbone_form inference = pvnet_amd.network.PVNetInference (BN folded; MIOpen "
                      "convolutions, each followed by one HIP epilogue pass for bias / residual / activation / the cat "
-                     "after fc; HIP upsample+cat; convraw's LeakyReLU + 1x1 conv as one matrix-core pass); the "
-                     "backbone alone is a separate graph")
+                     "after fc; HIP upsample+cat; fp16: the decoder tail up2 + cat([fm, x]) + convraw (3x3 conv, "
+                     "LeakyReLU, 1x1 conv) as one matrix-core kernel, pv_decoder_tail_f16; f32: convraw's LeakyReLU "
+                     "+ 1x1 conv as one matrix-core pass); the backbone alone is a separate graph")
 
 
 def measure_kp_vs_ref(dev):

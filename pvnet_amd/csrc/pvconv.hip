@@ -74,7 +74,18 @@ struct TailArgs {
     _Float16 *out;         // [N][H][W][cout]
     int N, Hin, Win, H, W, tiles_r, tiles_c, ntiles;
     float rh, rw, slope;
+#ifdef PVT_TRACE
+    unsigned long long *trace;   // [block][tile iteration < 8][wave][8 phase stamps] (s_memtime)
+#endif
 };
+
+#ifdef PVT_TRACE
+#define PVT_STAMP(k)                                                                                      \
+    if (a.trace && it < 8 && lane == 0)                                                                 \
+        a.trace[(((int64_t)blockIdx.x * 8 + it) * 4 + wid) * 8 + (k)] = __builtin_amdgcn_s_memtime()
+#else
+#define PVT_STAMP(k)
+#endif
 
 __device__ __forceinline__ void tile_coords(const TailArgs &a, int tile, int &b, int &y0, int &x0, int &ly0,
                                             int &lx0) {
@@ -87,29 +98,109 @@ __device__ __forceinline__ void tile_coords(const TailArgs &a, int tile, int &b,
     lx0 = (int)(a.rw * (float)max(x0 - 1, 0));
 }
 
-// global loads of a tile's fm patch and image rows into registers, branch-free:
-// addresses are clamped into the maps (the halo build never reads a patch
-// pixel outside fm, and writes zeros itself for halo pixels outside the
-// image), so nothing waits on the loads until the next tile's halo build.
-// pk / ik: the thread's tile-independent chunk coordinates (hoisted).
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+
+// buffer descriptor over one image's map: offsets past `bytes` (and, as
+// unsigned, negative ones) read 0 / drop the store -- the fetches need no clamps
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t image_rsrc(const void *base, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)bytes, 0x00020000);
+}
+
+// global loads of a tile's fm patch and image rows into registers (buffer
+// loads: rows past the map read 0, columns past it read the next row -- the
+// halo build never uses either), so nothing waits on them until the next
+// tile's halo build.  pk / ik: the thread's tile-independent chunk coordinates.
 __device__ __forceinline__ void fetch(const TailArgs &a, int tile, const int (&pk)[kPatchIt],
                                       const int (&ik)[kImgIt], h8 (&pre)[kPatchIt], uint32_t (&pimg)[kImgIt]) {
     int b, y0, x0, ly0, lx0;
     tile_coords(a, tile, b, y0, x0, ly0, lx0);
-    const _Float16 *fmb = a.fm + (int64_t)b * a.Hin * a.Win * 32;
+    const int64_t fbytes = (int64_t)a.Hin * a.Win * 64;
+    const __amdgpu_buffer_rsrc_t fr = image_rsrc(a.fm + (int64_t)b * a.Hin * a.Win * 32, fbytes);
+    const int base = (ly0 * a.Win + lx0) * 64;
 #pragma unroll
     for (int i = 0; i < kPatchIt; ++i) {
-        const int row = min(ly0 + (pk[i] >> 16), a.Hin - 1), col = min(lx0 + ((pk[i] >> 8) & 255), a.Win - 1);
-        pre[i] = *(const h8 *)(fmb + (row * a.Win + col) * 32 + 8 * (pk[i] & 3));
+        const int off = base + (pk[i] >> 16) * a.Win * 64 + (pk[i] & 0xffff);
+        pre[i] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(fr, off, 0, 0));
     }
-    const uint32_t *imb = (const uint32_t *)(a.img + (int64_t)b * a.H * a.W * 3);
-    const int rowdw = a.W * 3 / 2;                 // dwords per image row (W even)
+    const int64_t ibytes = (int64_t)a.H * a.W * 6;
+    const __amdgpu_buffer_rsrc_t ir = image_rsrc(a.img + (int64_t)b * a.H * a.W * 3, ibytes);
+    const int ibase = ((y0 - 1) * a.W * 3 / 2 + x0 * 3 / 2 - 2) * 4;
 #pragma unroll
     for (int i = 0; i < kImgIt; ++i) {
-        const int oy = min(max(y0 - 1 + (ik[i] >> 8), 0), a.H - 1);
-        const int j = min(max(x0 * 3 / 2 - 2 + (ik[i] & 255), 0), rowdw - 1);
-        pimg[i] = imb[oy * rowdw + j];
+        const int off = ibase + (ik[i] >> 8) * a.W * 6 + (ik[i] & 255) * 4;
+        pimg[i] = __builtin_amdgcn_raw_buffer_load_b32(ir, off, 0, 0);
     }
+}
+
+// per-thread fixed task geometry of the halo build (tile independent): the
+// 136 (halo column, 8-channel group) pairs c = 4 hx + q over the halo's 10
+// rows (row blends) and the patch's 7 rows (column blends)
+struct Geo {
+    int rc0, rhy0, rc1, rhy1;    // row blends: rows rhy0 .. rhy0 + 4 of column task rc0; + (rc1, rhy1) if rx
+    bool rx;
+    int tc0, tr0, tn0, tc1, tr1;  // column blends: rows tr0 .. tr0 + tn0 - 1 of tc0; + (tc1, tr1) if tx
+    bool tx;
+};
+
+__device__ __forceinline__ Geo make_geo(int t) {
+    Geo g;
+    const bool lo = t < 136;
+    g.rc0 = lo ? t : t - 136;          // 136 + 120 threads x 5 rows; the last 16 columns of rows 5..9
+    g.rhy0 = lo ? 0 : 5;               // by threads 0..79
+    g.rx = t < 80;
+    g.rc1 = 120 + (t & 15);
+    g.rhy1 = 5 + (t >> 4);
+    g.tc0 = g.rc0;                     // 136 threads x rows 0..3, 120 x rows 4..6; the last 16 columns
+    g.tr0 = lo ? 0 : 4;                // of rows 4..6 by threads 136..183
+    g.tn0 = lo ? 4 : 3;
+    g.tx = t >= 136 && t < 184;
+    g.tc1 = 120 + ((t - 136) & 15);
+    g.tr1 = 4 + ((t - 136) >> 4);
+    return g;
+}
+
+// column blend for task column c of the tile: the patch offset of its left
+// source pixel, the right one's distance, and the weights (fp16)
+struct ColW {
+    int poff, dp;
+    _Float16 w0, w1;
+};
+
+__device__ __forceinline__ ColW col_weights(const TailArgs &a, int c, int x0, int lx0) {
+    const int hx = c >> 2;
+    const int ox = min(max(x0 - 1 + hx, 0), a.W - 1);
+    const float w1r = a.rw * (float)ox;
+    const int w1 = (int)w1r;
+    const float w1l = w1r - (float)w1;
+    ColW r;
+    r.poff = (w1 - lx0) * 32 + 8 * (c & 3);
+    r.dp = w1 < a.Win - 1 ? 32 : 0;
+    r.w0 = (_Float16)(1.f - w1l);
+    r.w1 = (_Float16)w1l;
+    return r;
+}
+
+__device__ __forceinline__ void col_blend(const _Float16 *patch, _Float16 *tcol, const ColW &w, int c, int r) {
+    const _Float16 *p = patch + r * (kPC * 32) + w.poff;
+    const h8 A = *(const h8 *)p, B = *(const h8 *)(p + w.dp);
+    *(h8 *)(tcol + r * (kHC * 32) + 8 * c) = __builtin_elementwise_fma(B, (h8)w.w1, A * (h8)w.w0);
+}
+
+__device__ __forceinline__ void row_blend(const TailArgs &a, const _Float16 *tcol, _Float16 *halo, int c, int hy,
+                                          bool colok, int y0, int ly0) {
+    const int oy = y0 - 1 + hy;
+    h8 v = {};
+    if (colok && oy >= 0 && oy < a.H) {
+        const float h1r = a.rh * (float)oy;
+        const int h1 = (int)h1r;
+        const int dh = h1 < a.Hin - 1 ? kHC * 32 : 0;
+        const float h1l = h1r - (float)h1;
+        const _Float16 *tp = tcol + (h1 - ly0) * (kHC * 32) + 8 * c;
+        const h8 c0 = *(const h8 *)tp, c1 = *(const h8 *)(tp + dh);
+        v = __builtin_elementwise_fma(c1, (h8)(_Float16)h1l, c0 * (h8)(_Float16)(1.f - h1l));
+    }
+    *(h8 *)(halo + hy * (kHC * kCP) + (c >> 2) * kCP + 8 * (c & 3)) = v;
 }
 
 template <int COUT>
@@ -144,7 +235,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int i = 0; i < kPatchIt; ++i) {
         const int c = min((int)threadIdx.x + 256 * i, kPatchChunks - 1);
         const int pp = c >> 2, pr = pp / kPC;
-        pk[i] = (pr << 16) | ((pp - pr * kPC) << 8) | (c & 3);
+        pk[i] = (pr << 16) | ((pp - pr * kPC) * 64 + 16 * (c & 3));
     }
 #pragma unroll
     for (int i = 0; i < kImgIt; ++i) {
@@ -152,15 +243,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         const int r = w / kImgDw;
         ik[i] = (r << 8) | (w - r * kImgDw);
     }
+    const Geo g = make_geo((int)threadIdx.x);
     // next tile's inputs, fetched during this tile's convolution
     h8 pre[kPatchIt];
     uint32_t pimg[kImgIt];
     int tile = (int)blockIdx.x;
     if (tile < a.ntiles) fetch(a, tile, pk, ik, pre, pimg);
-    for (; tile < a.ntiles; tile += (int)gridDim.x) {
+    for (int it = 0; tile < a.ntiles; tile += (int)gridDim.x, ++it) {
+        (void)it;
+        PVT_STAMP(0);
         int b, y0, x0, ly0, lx0;
         tile_coords(a, tile, b, y0, x0, ly0, lx0);
-        __syncthreads();   // the previous tile's halo reads are done
+        // patch / imgs were last read before the previous tile's second barrier
 #pragma unroll
         for (int i = 0; i < kPatchIt; ++i) {
             const int c = (int)threadIdx.x + 256 * i;
@@ -171,54 +265,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             const int w = (int)threadIdx.x + 256 * i;
             if (w < kImgWords) imgs[w] = pimg[i];
         }
+        PVT_STAMP(1);
         __syncthreads();
-        // ---- halo: pixel (y0 - 1 + hy, x0 - 1 + hx) ----
+        PVT_STAMP(2);
+        // ---- halo: pixel (y0 - 1 + hy, x0 - 1 + hx).  x2 bilinear, align_corners, separably:
+        // column blends t = w0l A + w1l B per (fm row, halo column, 8 channels) ----
 #ifndef PVT_SKIP_HALO
-        // column blends t = w0l A + w1l B per (fm row r, halo column hx, 8 channels)
-        for (int task = (int)threadIdx.x; task < kTcolTasks; task += 256) {
-            const int q = task & 3, rc = task >> 2;
-            const int r = rc / kHC, hx = rc - r * kHC;
-            const int ox = min(max(x0 - 1 + hx, 0), a.W - 1);
-            const float w1r = a.rw * (float)ox;
-            const int w1 = (int)w1r, w1p = w1 < a.Win - 1 ? 32 : 0;
-            const float w1l = w1r - (float)w1;
-            const _Float16 *p = patch + (r * kPC + (w1 - lx0)) * 32 + 8 * q;
-            const h8 A = *(const h8 *)p, B = *(const h8 *)(p + w1p);
-            *(h8 *)(tcol + 8 * task) =
-                __builtin_elementwise_fma(B, (h8)(_Float16)w1l, A * (h8)(_Float16)(1.f - w1l));
-        }
-        // the image's channels 32..39 (3 + 5 zero)
-        for (int p = (int)threadIdx.x; p < kHaloPx; p += 256) {
-            const int hy = p / kHC, hx = p - hy * kHC;
-            const int oy = y0 - 1 + hy, ox = x0 - 1 + hx;
-            h8 v = {};
-            if (oy >= 0 && oy < a.H && ox >= 0 && ox < a.W) {
-                const uint16_t *ip = (const uint16_t *)(imgs + hy * kImgDw) + 3 * hx + 1;
-                v[0] = __builtin_bit_cast(_Float16, ip[0]);
-                v[1] = __builtin_bit_cast(_Float16, ip[1]);
-                v[2] = __builtin_bit_cast(_Float16, ip[2]);
-            }
-            *(h8 *)(halo + p * kCP + 32) = v;
-        }
-        __syncthreads();
-        // row blends h0l t(h1) + h1l t(h1 + 1) per (halo pixel, 8 channels)
-        for (int task = (int)threadIdx.x; task < kHaloPx * 4; task += 256) {
-            const int q = task & 3, px = task >> 2;
-            const int hy = px / kHC, hx = px - hy * kHC;
-            const int oy = y0 - 1 + hy, ox = x0 - 1 + hx;
-            h8 v = {};
-            if (oy >= 0 && oy < a.H && ox >= 0 && ox < a.W) {
-                const float h1r = a.rh * (float)oy;
-                const int h1 = (int)h1r, h1p = h1 < a.Hin - 1 ? kHC * 32 : 0;
-                const float h1l = h1r - (float)h1;
-                const _Float16 *tp = tcol + ((h1 - ly0) * kHC + hx) * 32 + 8 * q;
-                const h8 c0 = *(const h8 *)tp, c1 = *(const h8 *)(tp + h1p);
-                v = __builtin_elementwise_fma(c1, (h8)(_Float16)h1l, c0 * (h8)(_Float16)(1.f - h1l));
-            }
-            *(h8 *)(halo + px * kCP + 8 * q) = v;
+        {
+            const ColW w0 = col_weights(a, g.tc0, x0, lx0);
+            for (int i = 0; i < g.tn0; ++i) col_blend(patch, tcol, w0, g.tc0, g.tr0 + i);
+            if (g.tx) col_blend(patch, tcol, col_weights(a, g.tc1, x0, lx0), g.tc1, g.tr1);
         }
 #endif
+        PVT_STAMP(3);
+        __syncthreads();   // also: every wave is past the previous tile's convolution (halo reads)
+        PVT_STAMP(4);
+#ifndef PVT_SKIP_HALO
+        {
+            // row blends h0l t(h1) + h1l t(h1 + 1) per (halo pixel, 8 channels)
+            const int ox0 = x0 - 1 + (g.rc0 >> 2), ox1 = x0 - 1 + (g.rc1 >> 2);
+            const bool ok0 = ox0 >= 0 && ox0 < a.W, ok1 = ox1 >= 0 && ox1 < a.W;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) row_blend(a, tcol, halo, g.rc0, g.rhy0 + i, ok0, y0, ly0);
+            if (g.rx) row_blend(a, tcol, halo, g.rc1, g.rhy1, ok1, y0, ly0);
+            // the image's channels 32..39 (3 + 5 zero)
+            for (int p = (int)threadIdx.x; p < kHaloPx; p += 256) {
+                const int hy = p / kHC, hx = p - hy * kHC;
+                const int oy = y0 - 1 + hy, ox = x0 - 1 + hx;
+                h8 v = {};
+                if (oy >= 0 && oy < a.H && ox >= 0 && ox < a.W) {
+                    const uint16_t *ip = (const uint16_t *)(imgs + hy * kImgDw) + 3 * hx + 1;
+                    v[0] = __builtin_bit_cast(_Float16, ip[0]);
+                    v[1] = __builtin_bit_cast(_Float16, ip[1]);
+                    v[2] = __builtin_bit_cast(_Float16, ip[2]);
+                }
+                *(h8 *)(halo + p * kCP + 32) = v;
+            }
+        }
+#endif
+        PVT_STAMP(5);
         __syncthreads();
+        PVT_STAMP(6);
         if (tile + (int)gridDim.x < a.ntiles) fetch(a, tile + (int)gridDim.x, pk, ik, pre, pimg);
         // ---- the wave's two output rows: 3x3 convolution on the matrix cores ----
         f16x acc[2];
@@ -244,52 +331,58 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #else
         acc[0][0] = (float)halo[threadIdx.x];
 #endif
+        PVT_STAMP(7);
         // ---- epilogue + head, per row ----
+        const __amdgpu_buffer_rsrc_t orr =
+            image_rsrc(a.out + (int64_t)b * a.H * a.W * COUT, (int64_t)a.H * a.W * COUT * 2);
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
             const int oy = y0 + 2 * wid + r, ox = x0 + n;
             // conv rows of acc[i]: (i & 3) + 8 (i >> 2) + 4 h -- 4 consecutive rows per i >> 2
             h8 act[2];
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const h4 bq = *(const h4 *)(bias + 8 * g + 4 * h);
+            for (int gq = 0; gq < 4; ++gq) {
+                const h4 bq = *(const h4 *)(bias + 8 * gq + 4 * h);
                 h4 y;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) y[j] = (_Float16)acc[r][4 * g + j];   // the conv's fp16 output
+                for (int j = 0; j < 4; ++j) y[j] = (_Float16)acc[r][4 * gq + j];   // the conv's fp16 output
                 y = y + bq;
                 h4 ys;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) ys[j] = (_Float16)((float)y[j] * a.slope);
                 y = __builtin_elementwise_max(y, ys);          // LeakyReLU, slope < 1
 #pragma unroll
-                for (int j = 0; j < 4; ++j) act[g >> 1][4 * (g & 1) + j] = y[j];
+                for (int j = 0; j < 4; ++j) act[gq >> 1][4 * (gq & 1) + j] = y[j];
             }
+            // byte offset of the pixel's outputs; past the buffer (dropped) outside the image
+            const int po = (oy < a.H && ox < a.W) ? (oy * a.W + ox) * (COUT * 2) : (int)0x80000000;
 #pragma unroll
             for (int t = 0; t < MT; ++t) {
                 f16x d = {};
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) d = __builtin_amdgcn_mfma_f32_32x32x16_f16(wb[t][s2], act[s2], d, 0, 0, 0);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int o0 = 32 * t + 8 * q + 4 * h;
+                    if (o0 + 3 < COUT) {
+                        h4 v;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) v[j] = (_Float16)d[4 * q + j];
+                        v = v + *(const h4 *)(bias + 32 + o0);
 #ifdef PVT_SKIP_STORE
-                if (oy < a.H && ox < a.W && d[0] == 1234.5f) {
-#else
-                if (oy < a.H && ox < a.W) {
+                        if (v[0] == (_Float16)1234.5f)
 #endif
-                    _Float16 *op = a.out + (((int64_t)b * a.H + oy) * a.W + ox) * COUT;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int o0 = 32 * t + 8 * q + 4 * h;
-                        if (o0 + 3 < COUT) {
-                            h4 v;
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) v[j] = (_Float16)d[4 * q + j];
-                            *(h4 *)(op + o0) = v + *(const h4 *)(bias + 32 + o0);
-                        }
+                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), orr, po + 2 * o0, 0, 0);
                     }
                 }
             }
         }
     }
 }
+
+#ifdef PVT_TRACE
+unsigned long long *g_tail_trace = nullptr;
+#endif
 
 int cu_count_dec() {
     static int n = 0;
@@ -324,7 +417,8 @@ extern "C" int pv_decoder_tail_f16(const void *fm, const void *img, const void *
     a.out = (_Float16 *)out;
     a.N = n; a.Hin = hin; a.Win = win; a.H = 2 * hin; a.W = 2 * win;
     if ((int64_t)n * a.H * a.W * 40 >= (1ll << 31) * 16) return PV_EINVAL;
-    if ((int64_t)a.H * a.W * 3 >= (1ll << 31) || (int64_t)hin * win * 32 >= (1ll << 31)) return PV_EINVAL;
+    // one image's map per buffer descriptor (32-bit byte offsets)
+    if ((int64_t)a.H * a.W * 2 * cout >= (1ll << 31) || (int64_t)hin * win * 64 >= (1ll << 31)) return PV_EINVAL;
     a.tiles_r = (a.H + kTR - 1) / kTR;
     a.tiles_c = (a.W + kTC - 1) / kTC;
     const int64_t nt = (int64_t)n * a.tiles_r * a.tiles_c;
@@ -334,6 +428,9 @@ extern "C" int pv_decoder_tail_f16(const void *fm, const void *img, const void *
     a.rh = (float)(hin - 1) / (float)(a.H - 1);
     a.rw = (float)(win - 1) / (float)(a.W - 1);
     a.slope = slope;
+#ifdef PVT_TRACE
+    a.trace = g_tail_trace;
+#endif
     const int64_t grid = std::min<int64_t>(nt, 2ll * cu_count_dec());   // persistent: 2 blocks per CU
     hipStream_t s = (hipStream_t)stream;
     if (cout == 20) k_decoder_tail<20><<<(unsigned)grid, 256, 0, s>>>(a);
@@ -341,3 +438,7 @@ extern "C" int pv_decoder_tail_f16(const void *fm, const void *img, const void *
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? PV_OK : (int)e;
 }
+
+#ifdef PVT_TRACE
+extern "C" void pv_debug_set_tail_trace(void *p) { g_tail_trace = (unsigned long long *)p; }
+#endif
