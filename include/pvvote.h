@@ -234,6 +234,16 @@ int pv_conv_epilogue_f16(const void *x, const void *bias, const void *res, const
 int pv_conv_epilogue_f32(const void *x, const void *bias, const void *res, const void *rbias, const void *skip,
                          void *out, int64_t P, int32_t c1, int32_t c2, int32_t act, float slope, pv_stream_t stream);
 
+/* replaces the stem's tail (lib/networks/resnet.py:201-204: relu(bn1(conv1(x))) = x2s, then
+ * maxpool 3x3 / stride 2 / pad 1) for channels-last maps, BN folded into bias: x2s = relu(x + bias)
+ * [n][h][w][c] and pool = maxpool(x2s) [n][(h-1)/2+1][(w-1)/2+1][c] in one pass.  x: the convolution's
+ * output without bias; bias [c]; fp16: c a multiple of 8, f32: of 4; pointers 16-byte aligned, the three
+ * maps distinct.  Both outputs equal ATen's bias add + ReLU + max_pool2d bit for bit. */
+int pv_relu_maxpool_f16(const void *x, const void *bias, void *x2s, void *pool, int32_t n, int32_t h, int32_t w,
+                        int32_t c, pv_stream_t stream);
+int pv_relu_maxpool_f32(const void *x, const void *bias, void *x2s, void *pool, int32_t n, int32_t h, int32_t w,
+                        int32_t c, pv_stream_t stream);
+
 /* replaces convraw's tail (model_repository.py:53-58 after the 3x3 convolution): BN bias + LeakyReLU(slope)
  * + the 1x1 convolution to seg_dim + ver_dim channels with its bias, one pass.  x: [P][cin] channels-last
  * (the 3x3 convolution's output without bias), b1 f32 [cin], w2 f32 [cout][cin], b2 f32 [cout] (device),

@@ -164,6 +164,73 @@ int epilogue(const void *x, const void *bias, const void *res, const void *rbias
 }
 
 // --------------------------------------------------------------------------
+// The stem's tail (RN:139-142 conv1 -> bn1 -> relu = x2s, then maxpool
+// 3x3 / 2 / pad 1; RN:201-204): x2s = relu(x + b) written once and the pooled
+// map from it in the same pass.  Thread = 16 bytes of channels of one pooled
+// pixel: it reads its 3x3 window of the conv output, writes the 2x2 of x2s it
+// owns (rows 2py, 2py + 1, columns 2px, 2px + 1 -- the owned blocks tile x2s)
+// and the window's max.  Roundings as k_epilogue; the max is exact, so both
+// maps equal ATen's bias add + ReLU + max_pool2d bit for bit.
+// --------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void k_relu_pool(const T *__restrict__ x, const T *__restrict__ bias,
+                                                   T *__restrict__ x2s, T *__restrict__ pool, int N, int H, int W,
+                                                   int C, int Ho, int Wo) {
+    constexpr int V = 16 / sizeof(T);
+    typedef typename Vec<T, V>::type vT;
+    const int cv = C / V;
+    const int64_t total = (int64_t)N * Ho * Wo * cv;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int k = (int)(i % cv);
+        const int64_t p = i / cv;
+        const int px = (int)(p % Wo);
+        const int64_t q = p / Wo;
+        const int py = (int)(q % Ho), b = (int)(q / Ho);
+        const vT bv = *(const vT *)(bias + V * k);
+        vT m;
+#pragma unroll
+        for (int e = 0; e < V; ++e) m[e] = (T)(-INFINITY);
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy) {
+            const int iy = 2 * py + dy;
+            if (iy < 0 || iy >= H) continue;
+#pragma unroll
+            for (int dx = -1; dx <= 1; ++dx) {
+                const int ix = 2 * px + dx;
+                if (ix < 0 || ix >= W) continue;
+                const int64_t off = (((int64_t)b * H + iy) * W + ix) * C + V * k;
+                vT v = *(const vT *)(x + off);
+#pragma unroll
+                for (int e = 0; e < V; ++e) {
+                    const T y = (T)((float)v[e] + (float)bv[e]);
+                    v[e] = (float)y > 0.f ? y : (T)0.f;
+                    m[e] = (float)v[e] > (float)m[e] ? v[e] : m[e];
+                }
+                if (dy >= 0 && dx >= 0) *(vT *)(x2s + off) = v;
+            }
+        }
+        *(vT *)(pool + p * C + V * k) = m;
+    }
+}
+
+template <typename T>
+int relu_pool(const void *x, const void *bias, void *x2s, void *pool, int32_t n, int32_t h, int32_t w, int32_t c,
+              pv_stream_t stream) {
+    constexpr int V = 16 / sizeof(T);
+    if (!x || !bias || !x2s || !pool || n < 0 || h <= 0 || w <= 0 || c <= 0 || c % V) return PV_EINVAL;
+    if (((uintptr_t)x | (uintptr_t)bias | (uintptr_t)x2s | (uintptr_t)pool) % 16) return PV_EALIGN;
+    if (x2s == x || pool == x || pool == x2s) return PV_EINVAL;
+    if (n == 0) return PV_OK;
+    const int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;     // kernel 3, stride 2, pad 1
+    const int64_t total = (int64_t)n * ho * wo * (c / V);
+    const int64_t blocks = (total + 255) / 256;
+    k_relu_pool<T><<<(unsigned)(blocks < 256 * 64 ? blocks : 256 * 64), 256, 0, (hipStream_t)stream>>>(
+        (const T *)x, (const T *)bias, (T *)x2s, (T *)pool, n, h, w, c, ho, wo);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? PV_OK : (int)e;
+}
+
+// --------------------------------------------------------------------------
 // The network's head, convraw after its 3x3 convolution (MR:53-58): the
 // folded BN bias + LeakyReLU(0.1) and the 1x1 convolution to seg_dim +
 // ver_dim channels with its bias, in one pass -- 32 channels in, 20 (or 44,
@@ -322,4 +389,14 @@ extern "C" int pv_upsample2x_cat_f16(const void *x, const void *skip, void *out,
 extern "C" int pv_upsample2x_cat_f32(const void *x, const void *skip, void *out, int32_t n, int32_t hin,
                                      int32_t win, int32_t c1, int32_t c2, int32_t cpad, pv_stream_t stream) {
     return up2_cat<float>(x, skip, out, n, hin, win, c1, c2, cpad, stream);
+}
+
+extern "C" int pv_relu_maxpool_f16(const void *x, const void *bias, void *x2s, void *pool, int32_t n, int32_t h,
+                                   int32_t w, int32_t c, pv_stream_t stream) {
+    return relu_pool<_Float16>(x, bias, x2s, pool, n, h, w, c, stream);
+}
+
+extern "C" int pv_relu_maxpool_f32(const void *x, const void *bias, void *x2s, void *pool, int32_t n, int32_t h,
+                                   int32_t w, int32_t c, pv_stream_t stream) {
+    return relu_pool<float>(x, bias, x2s, pool, n, h, w, c, stream);
 }

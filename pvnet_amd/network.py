@@ -246,6 +246,21 @@ def head(y: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor, 
     return out
 
 
+def relu_maxpool(y: torch.Tensor, bias: torch.Tensor):
+    """The stem's tail (RN:201-204) after conv1, BN folded: x2s = relu(y +
+    bias) and maxpool3x3/2/1(x2s) from one HIP pass (``pv_relu_maxpool_f16 /
+    _f32``), both bit-equal to ATen's ops.  y [n, c, h, w] channels_last."""
+    n, c, h, w = y.shape
+    cl = torch.channels_last
+    if not y.is_contiguous(memory_format=cl):
+        raise RuntimeError("relu_maxpool: channels_last input required")
+    x2s = torch.empty_like(y, memory_format=cl)
+    pool = torch.empty((n, c, (h - 1) // 2 + 1, (w - 1) // 2 + 1), dtype=y.dtype, device=y.device, memory_format=cl)
+    _dev_call("pv_relu_maxpool_f16", "pv_relu_maxpool_f32", y, y.data_ptr(), bias.data_ptr(), x2s.data_ptr(),
+              pool.data_ptr(), n, h, w, c)
+    return x2s, pool
+
+
 def decoder_tail_weights(c0: nn.Conv2d, c1: nn.Conv2d, cin: int = 35):
     """convraw's weights (MR:53-58, BN folded into ``c0``) laid out for
     ``pv_decoder_tail_f16`` (include/pvvote.h): w1 [32][368] fp16 with
@@ -352,8 +367,12 @@ class PVNetInference(nn.Module):
 
     def forward(self, x):
         r = self.resnet18_8s
-        x2s = conv_epilogue(_conv(x, r.conv1), r.conv1.bias, "relu")
-        y = r.maxpool(x2s)
+        mp = r.maxpool
+        if (mp.kernel_size, mp.stride, mp.padding, mp.dilation, mp.ceil_mode) == (3, 2, 1, 1, False):
+            x2s, y = relu_maxpool(_conv(x, r.conv1), r.conv1.bias)
+        else:
+            x2s = conv_epilogue(_conv(x, r.conv1), r.conv1.bias, "relu")
+            y = mp(x2s)
         for blk in r.layer1:
             y = self._block(blk, y)
         x4s = y

@@ -465,3 +465,21 @@ def test_decoder_tail_matches_torch(cout, hw, device):
           f"mean {float(d.mean()):.3e} (tolerance {tol:.3e}, scale {sc:.2f})")
     assert float(d.max()) <= tol
     assert float(d.mean()) <= 2 ** -12 * sc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
+@pytest.mark.parametrize("hw", [(24, 40), (23, 17)])
+def test_relu_maxpool_matches_torch(dtype, hw, device):
+    """pv_relu_maxpool (the stem's bias + ReLU = x2s and maxpool 3x3/2/1,
+    RN:201-204) equals ATen's ops bit for bit, odd sizes included."""
+    from pvnet_amd.network import relu_maxpool
+    g = torch.Generator().manual_seed(hw[0] * 100 + hw[1])
+    cl = torch.channels_last
+    y = (torch.randn(3, 64, *hw, generator=g) * 3).to(device, dtype).contiguous(memory_format=cl)
+    b = torch.randn(64, generator=g).to(device, dtype)
+    ref_x2s = torch.relu(y + b.view(1, -1, 1, 1))
+    ref_pool = torch.nn.functional.max_pool2d(ref_x2s, 3, 2, 1)
+    x2s, pool = relu_maxpool(y, b)
+    assert x2s.is_contiguous(memory_format=cl) and pool.is_contiguous(memory_format=cl)
+    assert torch.equal(x2s, ref_x2s) and torch.equal(pool, ref_pool)
