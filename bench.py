@@ -41,8 +41,9 @@ FP32_VECTOR_PEAK_TFLOPS = 157.3
 H, W, VN = 480, 640, 9
 
 
-PMC_FILE = "profiles/r02_pmc_traffic.json"
-STATS_FILE = "profiles/r02_bench_kernel_stats.csv"
+PMC_FILE = "profiles/r03_pmc_traffic.json"
+U1_WARM, U1_TIMED = 5, 3            # measure_u1: graph replays (of 100 launches) untimed, then timed
+STATS_FILE = "profiles/r03_bench_kernel_stats.csv"
 
 
 def pmc_traffic(kernel):
@@ -332,9 +333,9 @@ def _raw_v3(rvg, seg, ver, hn, seed, work, out, dd):
 def measure_u1(dev, hn=512, reps=100):
     """API-faithful voting_for_hypothesis (dense u8 [hn,vn,tn] write) on one
     S(1234) image: the kernel the north star's HBM roofline names (U1).
-    Timed on the launching stream with hipEvents around one replay of a
-    hipGraph of `reps` back-to-back calls: the device time per call in the
-    steady state, where each launch's 137.6 MB drain to HBM behind the next
+    Timed on the launching stream with hipEvents around U1_TIMED replays of a
+    hipGraph of `reps` calls, queued behind U1_WARM untimed ones: the device
+    time per call in the sustained steady state, where each launch's 137.6 MB drain to HBM behind the next
     one (a launch alone on an idle device partly lands in the 256 MiB
     Infinity Cache and measures faster); rocprof's kernel trace of the same
     command times these launches (the only other ones are the 5 warm-up calls)."""
@@ -356,8 +357,7 @@ def measure_u1(dev, hn=512, reps=100):
             rv.voting_for_hypothesis_dense(direct, coords, hyp, inl, 0.99)
     torch.cuda.synchronize()
     # `reps` launches back to back in one hipGraph (no host gaps between
-    # them: the device time per launch that rocprof's kernel trace measures,
-    # plus the graph's dispatch gap), events around one replay
+    # them: the device time per launch that rocprof's kernel trace measures)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.stream(s):
         with torch.cuda.graph(g, stream=s):
@@ -365,13 +365,21 @@ def measure_u1(dev, hn=512, reps=100):
                 rv.voting_for_hypothesis_dense(direct, coords, hyp, inl, 0.99)
     g.replay()
     torch.cuda.synchronize()
+    # sustained: U1_WARM replays back to back untimed (the clocks and the
+    # Infinity Cache reach their steady state: the first replays after an
+    # idle device run 36 -> 31 us per launch, tools/u1_replays.py), then
+    # U1_TIMED replays timed -- queued behind the warm ones, so the events
+    # see kernel after kernel, the period rocprof's trace shows
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     with torch.cuda.stream(s):
+        for _ in range(U1_WARM):
+            g.replay()
         a.record(s)
-        g.replay()
+        for _ in range(U1_TIMED):
+            g.replay()
         b.record(s)
     torch.cuda.synchronize()
-    ms = a.elapsed_time(b) / reps
+    ms = a.elapsed_time(b) / (reps * U1_TIMED)
     nbytes = 8 * tn * VN + 8 * tn + 8 * hn * VN + hn * VN * tn      # SURVEY 8(d) U1 algorithmic bytes
     return dict(kernel="k_vote_bytes<DENSE> (pv_voting_for_hypothesis)", bytes_per_launch=nbytes,
                 traffic=pmc_traffic("k_vote_bytes"), ms=ms,
@@ -775,9 +783,10 @@ def report(args, ws, res, final_err, dev):
                                     traffic=u1["traffic"], avg_kernel_ms=round(u1["ms"], 5),
                                     bytes_per_launch=u1["bytes_per_launch"], hn=u1["hn"], tn=u1["tn"],
                                     note="algorithmic bytes 8*tn*vn + 8*tn + 8*hn*vn + hn*vn*tn (SURVEY 8(d) U1) "
-                                         "per launch / avg_kernel_ms = hipEvents around one replay of a hipGraph of "
-                                         "100 back-to-back calls on the launching stream (each launch's writes "
-                                         "drain behind the next: the steady state); rocprof kernel durations of "
+                                         "per launch / avg_kernel_ms = hipEvents around 3 replays of a hipGraph of 100 "
+                                         "calls on the launching stream, queued behind 5 untimed replays (sustained "
+                                         "steady state: each launch's writes drain behind the next); rocprof kernel "
+                                         "durations of "
                                          "the same command: %s; "
                                          "traffic = 2*FETCH_SIZE + WRITE_SIZE per launch (%s)" % (STATS_FILE, PMC_FILE))
         except Exception as e:  # reported, never hides the main number

@@ -10,6 +10,7 @@ timeout -k 10 400 python3 $CMD > gpurun_out/bench_plain.log 2>&1 || { echo "benc
 grep '^{' gpurun_out/bench_plain.log | tail -1 > gpurun_out/bench_plain.json
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$PWD/gpurun_out/prof_bench" -o bench -- python3 $CMD > gpurun_out/bench_prof.log 2>&1 || { echo "prof failed"; tail -20 gpurun_out/bench_prof.log; exit 1; }
 grep '^{' gpurun_out/bench_prof.log | tail -1 > gpurun_out/bench_prof.json
+python3 tools/u1_trace_summary.py gpurun_out/prof_bench/bench_kernel_trace.csv gpurun_out/bench_prof.json gpurun_out/u1_timed_launches.json
 if [ -n "$PMC" ]; then
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 400 rocprofv3 --kernel-include-regex "k_vote|k_compact|k_fg_count|k_refine|k_hyp_gen|k_front" --pmc $c -T --output-format csv \
