@@ -384,6 +384,188 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 unsigned long long *g_tail_trace = nullptr;
 #endif
 
+
+// ==========================================================================
+// The backbone's wide 3x3 convolutions (layer3 / layer4 / fc: Cin a multiple
+// of 64, Cout a multiple of 256, stride 1, padding = dilation; RN:21-38,
+// 167-198, MR:22-26) as an implicit GEMM on v_mfma_f32_16x16x32_f16, with
+// the conv epilogue (folded BN bias, residual, ReLU; k_epilogue's roundings)
+// fused.  D[cout][pixel] = sum_k W[cout][k] X[k][pixel], k = tap * Cin + c.
+//
+// Block: 8 waves, a 256-cout x 256-pixel tile (wave = 128 couts x 64 pixels:
+// 8 x 4 accumulator tiles of 16 x 16, 128 VGPRs).  K-step = 64 (one tap, 64
+// input channels): the weights' and the pixels' 256 rows x 128 bytes each go
+// to LDS by buffer loads straight to LDS (16 bytes a lane; rows outside the
+// image or past the map read as zeros -- the convolution's zero padding),
+// two stages (128 KiB), the next step's loads in flight while this step's
+// 64 MFMAs per wave run; one barrier per step.  LDS image: row r's 16-byte
+// segment s at granule 8 r + (s ^ (r & 7)) (the XOR swizzle is applied to
+// the loads' source addresses; the LDS side is lane-linear), which keeps the
+// fragments' ds_read_b128 conflict-free.  The accumulator's 4 registers are
+// 4 consecutive output channels of one pixel: an 8-byte store per lane.
+// ==========================================================================
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+constexpr int kCT = 256;                   // couts per tile
+constexpr int kPT = 256;                   // pixels per tile
+constexpr int kStage = (kCT + kPT) * 128;  // bytes per stage (A then B), 64 KiB
+
+struct ConvArgs {
+    const _Float16 *x;      // [N][H][W][Cin]
+    const _Float16 *w;      // [Cout][9][Cin]
+    const _Float16 *bias;   // [Cout]
+    const _Float16 *res;    // [N][H][W][Cout] or null
+    const _Float16 *rbias;  // [Cout] or null
+    _Float16 *out;          // [N][H][W][Cout]
+    int N, H, W, Cin, Cout, ldo, dil, act, ntp, nct, ntiles, ksteps, cblocks;
+    float slope;
+    int64_t M;              // pixels
+};
+
+__global__ __launch_bounds__(512) void k_conv3x3(ConvArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kStage];
+    const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
+    // XCD-aware tile order: blocks i, i + 8, ... share an XCD; give each XCD a
+    // contiguous range of tiles, the cout tiles of a pixel tile adjacent
+    int bid = (int)blockIdx.x;
+    {
+        const int nb = (int)gridDim.x, q = nb / 8, r = nb % 8, x = bid % 8;
+        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+    }
+    const int ct = bid % a.nct, pt = bid / a.nct;
+    const int n0 = ct * kCT;
+    const int64_t p0 = (int64_t)pt * kPT;
+    const __amdgpu_buffer_rsrc_t wr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.w, 0, (int)((int64_t)a.Cout * 9 * a.Cin * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.x, 0, (int)(a.M * a.Cin * 2), 0x00020000);
+    const int K2 = 9 * a.Cin * 2;            // bytes per weight row
+    // this lane's 4 weight and 4 pixel granules per stage: granule g = (4 wid + i) 64 + lane
+    int woff[4], py[4], px[4];
+    int64_t pbase[4];
+    bool pin[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int g = (4 * wid + i) * 64 + lane, row = g >> 3, seg = (g & 7) ^ (row & 7);
+        woff[i] = (n0 + row) * K2 + seg * 16;
+        const int64_t p = p0 + row;
+        pin[i] = p < a.M;
+        const int64_t pc = pin[i] ? p : 0;
+        const int img = (int)(pc / ((int64_t)a.H * a.W)), rem = (int)(pc - (int64_t)img * a.H * a.W);
+        py[i] = rem / a.W;
+        px[i] = rem - py[i] * a.W;
+        pbase[i] = pc * a.Cin * 2 + seg * 16;
+    }
+    auto issue = [&](int s, int buf) {
+        const int tap = s / a.cblocks, cb = s - tap * a.cblocks;
+        const int dy = (tap / 3 - 1) * a.dil, dx = (tap % 3 - 1) * a.dil;
+        uint8_t *st = lds + buf * kStage;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                wr, (__attribute__((address_space(3))) void *)(st + (4 * wid + i) * 1024), 16, woff[i],
+                (tap * a.Cin + cb * 64) * 2, 0, 0);
+        const int dpix = (dy * a.W + dx) * a.Cin * 2 + cb * 128;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool ok = pin[i] && (unsigned)(py[i] + dy) < (unsigned)a.H && (unsigned)(px[i] + dx) < (unsigned)a.W;
+            const uint32_t off = ok ? (uint32_t)(pbase[i] + dpix) : 0x80000000u;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                xr, (__attribute__((address_space(3))) void *)(st + kCT * 128 + (4 * wid + i) * 1024), 16, off, 0, 0,
+                0);
+        }
+    };
+    const int wn = wid & 1, wm = wid >> 1;   // wave: couts wn*128 .. +127, pixels wm*64 .. +63
+    f4v acc[8][4];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f4v{0.f, 0.f, 0.f, 0.f};
+    issue(0, 0);
+    for (int s = 0; s < a.ksteps; ++s) {
+        const int buf = s & 1;
+        __builtin_amdgcn_s_waitcnt(0x0F70);          // this wave's loads of step s have landed (vmcnt 0)
+        __syncthreads();                              // ... and every wave's; step s-1's reads are done
+#ifdef PVC_NO_LOADS
+        if (s == 0 && a.ksteps > 1) issue(s + 1, buf ^ 1);
+#else
+        if (s + 1 < a.ksteps) issue(s + 1, buf ^ 1);
+#endif
+        const uint8_t *st = lds + buf * kStage;
+#pragma unroll
+        for (int kc = 0; kc < 2; ++kc) {
+            const int sg = kc * 4 + (lane >> 4);
+            h8v af[8], bf[4];
+#pragma unroll
+            for (int mi = 0; mi < 8; ++mi) {
+                const int r = wn * 128 + mi * 16 + (lane & 15);
+                af[mi] = *(const h8v *)(st + (r * 8 + (sg ^ (r & 7))) * 16);
+            }
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+                const int r = wm * 64 + ni * 16 + (lane & 15);
+                bf[ni] = *(const h8v *)(st + kCT * 128 + (r * 8 + (sg ^ (r & 7))) * 16);
+            }
+#ifdef PVC_NO_MFMA
+#pragma unroll
+            for (int mi = 0; mi < 8; ++mi) acc[mi][0][0] += (float)af[mi][0] + (float)bf[mi & 3][1];
+#else
+#pragma unroll
+            for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mi], bf[ni], acc[mi][ni], 0, 0, 0);
+#endif
+        }
+    }
+    // ---- epilogue: lane's accumulator (mi, ni) = couts c .. c+3 of pixel p;
+    // k_epilogue's roundings (bias add, residual (+ its bias), activation) ----
+    h4 bq[8], rbq[8];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+        const int c = n0 + wn * 128 + mi * 16 + 4 * (lane >> 4);
+        bq[mi] = *(const h4 *)(a.bias + c);
+        rbq[mi] = a.rbias ? *(const h4 *)(a.rbias + c) : h4{};
+    }
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+        const int64_t p = p0 + wm * 64 + ni * 16 + (lane & 15);
+        const bool pv = p < a.M;
+        const int64_t pc = pv ? p : 0;
+        h4 r[8];
+        if (a.res) {
+#pragma unroll
+            for (int mi = 0; mi < 8; ++mi)
+                r[mi] = *(const h4 *)(a.res + pc * a.Cout + n0 + wn * 128 + mi * 16 + 4 * (lane >> 4));
+        }
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) {
+            const int c = n0 + wn * 128 + mi * 16 + 4 * (lane >> 4);
+            h4 y;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) y[j] = (_Float16)((float)(_Float16)acc[mi][ni][j] + (float)bq[mi][j]);
+            if (a.res) {
+                h4 rr = r[mi];
+                if (a.rbias) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) rr[j] = (_Float16)((float)rr[j] + (float)rbq[mi][j]);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) y[j] = (_Float16)((float)y[j] + (float)rr[j]);
+            }
+            if (a.act == 1) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) y[j] = (float)y[j] > 0.f ? y[j] : (_Float16)0.f;
+            } else if (a.act == 2) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) y[j] = (float)y[j] > 0.f ? y[j] : (_Float16)((float)y[j] * a.slope);
+            }
+            if (pv) *(h4 *)(a.out + p * a.ldo + c) = y;
+        }
+    }
+}
+
 int cu_count_dec() {
     static int n = 0;
     if (!n) {
@@ -442,3 +624,32 @@ extern "C" int pv_decoder_tail_f16(const void *fm, const void *img, const void *
 #ifdef PVT_TRACE
 extern "C" void pv_debug_set_tail_trace(void *p) { g_tail_trace = (unsigned long long *)p; }
 #endif
+
+extern "C" int pv_conv3x3_f16(const void *x, const void *w, const void *bias, const void *res, const void *rbias,
+                              void *out, int32_t ldo, int32_t n, int32_t h, int32_t wd, int32_t cin, int32_t cout,
+                              int32_t dil, int32_t act, float slope, pv_stream_t stream) {
+    if (!x || !w || !bias || !out || n < 0 || h <= 0 || wd <= 0 || dil < 1 || act < 0 || act > 2) return PV_EINVAL;
+    if (cin <= 0 || cin % 64 || cout <= 0 || cout % kCT || (rbias && !res)) return PV_EINVAL;
+    if (ldo == 0) ldo = cout;
+    if (ldo < cout || ldo % 4) return PV_EINVAL;
+    if (((uintptr_t)x | (uintptr_t)w | (uintptr_t)out | (uintptr_t)res) % 16 || ((uintptr_t)bias | (uintptr_t)rbias) % 8)
+        return PV_EALIGN;
+    if (out == x || (res && out == res)) return PV_EINVAL;
+    if (n == 0) return PV_OK;
+    ConvArgs a;
+    a.x = (const _Float16 *)x; a.w = (const _Float16 *)w; a.bias = (const _Float16 *)bias;
+    a.res = (const _Float16 *)res; a.rbias = (const _Float16 *)rbias; a.out = (_Float16 *)out;
+    a.N = n; a.H = h; a.W = wd; a.Cin = cin; a.Cout = cout; a.ldo = ldo; a.dil = dil; a.act = act; a.slope = slope;
+    a.M = (int64_t)n * h * wd;
+    // 32-bit buffer offsets (+ the 0x80000000 out-of-range marker): the maps under 2 GiB
+    if (a.M * cin * 2 >= (1ll << 31) || (int64_t)cout * 9 * cin * 2 >= (1ll << 31) || a.M * ldo >= (1ll << 31))
+        return PV_EINVAL;
+    a.cblocks = cin / 64;
+    a.ksteps = 9 * a.cblocks;
+    a.ntp = (int)((a.M + kPT - 1) / kPT);
+    a.nct = cout / kCT;
+    a.ntiles = a.ntp * a.nct;
+    k_conv3x3<<<(unsigned)a.ntiles, 512, 0, (hipStream_t)stream>>>(a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? PV_OK : (int)e;
+}

@@ -261,6 +261,43 @@ def relu_maxpool(y: torch.Tensor, bias: torch.Tensor):
     return x2s, pool
 
 
+def conv3x3_eligible(c: nn.Conv2d) -> bool:
+    """The convolutions ``pv_conv3x3_f16`` takes: 3x3, stride 1, padding =
+    dilation, no groups, Cin a multiple of 64, Cout of 256 (layer3, layer4, fc)."""
+    return (c.kernel_size == (3, 3) and c.stride == (1, 1) and c.groups == 1 and c.padding == c.dilation
+            and c.dilation[0] == c.dilation[1] and c.in_channels % 64 == 0 and c.out_channels % 256 == 0)
+
+
+def conv3x3(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, dil: int, act: str = "relu",
+            res: torch.Tensor | None = None, rbias: torch.Tensor | None = None, slope: float = 0.1,
+            extra: int = 0) -> torch.Tensor:
+    """A wide 3x3 convolution and its epilogue, ``act(conv(x) + bias (+ (res
+    + rbias)))``, in one matrix-core pass (``pv_conv3x3_f16``): x [n, cin, h,
+    w] channels_last float16, w [cout, 3, 3, cin] contiguous (see
+    :func:`conv3x3_weight`), bias / rbias [cout] float16.  ``extra`` > 0:
+    the result is [n, cout + extra, h, w] with channels cout.. left for the
+    caller (the torch.cat after fc)."""
+    n, cin, h, wd = x.shape
+    cout = w.shape[0]
+    cl = torch.channels_last
+    if x.dtype != torch.float16 or not x.is_cuda or not x.is_contiguous(memory_format=cl):
+        raise RuntimeError("conv3x3: a channels_last float16 CUDA input is required")
+    if tuple(w.shape) != (cout, 3, 3, cin) or not w.is_contiguous() or w.dtype != torch.float16:
+        raise RuntimeError("conv3x3: weight [cout, 3, 3, cin] contiguous float16 required")
+    if res is not None and (tuple(res.shape) != (n, cout, h, wd) or not res.is_contiguous(memory_format=cl)):
+        raise RuntimeError("conv3x3: residual [n, cout, h, w] channels_last required")
+    out = torch.empty((n, cout + extra, h, wd), dtype=x.dtype, device=x.device, memory_format=cl)
+    _dev_call("pv_conv3x3_f16", None, x, x.data_ptr(), w.data_ptr(), bias.data_ptr(),
+              None if res is None else res.data_ptr(), None if rbias is None else rbias.data_ptr(), out.data_ptr(),
+              cout + extra, n, h, wd, cin, cout, int(dil), _ACT[act], float(slope))
+    return out
+
+
+def conv3x3_weight(c: nn.Conv2d) -> torch.Tensor:
+    """c's weight as pv_conv3x3_f16 reads it: [cout, 3, 3, cin], fp16, contiguous."""
+    return c.weight.detach().permute(0, 2, 3, 1).contiguous().half()
+
+
 def decoder_tail_weights(c0: nn.Conv2d, c1: nn.Conv2d, cin: int = 35):
     """convraw's weights (MR:53-58, BN folded into ``c0``) laid out for
     ``pv_decoder_tail_f16`` (include/pvvote.h): w1 [32][368] fp16 with
@@ -343,17 +380,38 @@ class PVNetInference(nn.Module):
         self.raw_in = c0.in_channels
         # fp16: convraw's input built and consumed inside one matrix-core kernel (decoder_tail)
         # when its shapes are the reference's (35 -> 32 -> 20 / 44); False = the MIOpen form
+        # fp16: layer3 / layer4 / fc's 3x3 convolutions + epilogues as pv_conv3x3_f16
+        self.fused_conv = True
         self.fused_tail = (c0.in_channels == 35 and c0.out_channels == 32 and f.convraw[3].out_channels in (20, 44)
                            and self.conv2s[0].out_channels == 32)
         self.eval()
 
+    def _wide(self, c: nn.Conv2d, x):
+        """fp16 and a wide 3x3 convolution (layer3, layer4, fc): the weight for
+        pv_conv3x3_f16, made once; else None (MIOpen + pv_conv_epilogue)."""
+        if not (self.fused_conv and x.dtype == torch.float16 and conv3x3_eligible(c)):
+            return None
+        key = (c.weight.data_ptr(), c.weight.dtype, c.weight._version)
+        cache = self.__dict__.setdefault("_wide_w", {})
+        hit = cache.get(id(c))
+        if hit is None or hit[0] != key:
+            hit = (key, conv3x3_weight(c))
+            cache[id(c)] = hit
+        return hit[1]
+
+    def _conv_act(self, c: nn.Conv2d, x, act, res=None, rbias=None):
+        w = self._wide(c, x)
+        if w is not None:
+            return conv3x3(x, w, c.bias, c.dilation[0], act, res=res, rbias=rbias)
+        return conv_epilogue(_conv(x, c), c.bias, act, res=res, rbias=rbias)
+
     def _block(self, blk: BasicBlock, x):
-        y = conv_epilogue(_conv(x, blk.conv1), blk.conv1.bias, "relu")
+        y = self._conv_act(blk.conv1, x, "relu")
         if blk.downsample is None:
             res, rb = x, None
         else:
             res, rb = _conv(x, blk.downsample[0]), blk.downsample[0].bias
-        return conv_epilogue(_conv(y, blk.conv2), blk.conv2.bias, "relu", res=res, rbias=rb)
+        return self._conv_act(blk.conv2, y, "relu", res=res, rbias=rb)
 
     def forward_modules(self, x):
         """The previous inference form (module epilogues: ATen bias / residual /
@@ -383,7 +441,13 @@ class PVNetInference(nn.Module):
             for blk in layer:
                 y = self._block(blk, y)
         # fc (conv + BN + ReLU, MR:22-26) and torch.cat([xfc, x8s], 1) (MR:66) in one epilogue
-        cat8 = conv_epilogue(_conv(y, r.fc[0]), r.fc[0].bias, "relu", skip=x8s)
+        wfc = self._wide(r.fc[0], y)
+        if wfc is not None:
+            c = r.fc[0]
+            cat8 = conv3x3(y, wfc, c.bias, c.dilation[0], "relu", extra=x8s.shape[1])
+            cat8[:, c.out_channels:].copy_(x8s)
+        else:
+            cat8 = conv_epilogue(_conv(y, r.fc[0]), r.fc[0].bias, "relu", skip=x8s)
         fm = conv_epilogue(_conv(cat8, self.conv8s[0]), self.conv8s[0].bias, "leaky")
         fm = upsample2x_cat(fm, x4s, fm.shape[1] + x4s.shape[1])
         fm = conv_epilogue(_conv(fm, self.conv4s[0]), self.conv4s[0].bias, "leaky")

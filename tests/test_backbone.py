@@ -483,3 +483,45 @@ def test_relu_maxpool_matches_torch(dtype, hw, device):
     x2s, pool = relu_maxpool(y, b)
     assert x2s.is_contiguous(memory_format=cl) and pool.is_contiguous(memory_format=cl)
     assert torch.equal(x2s, ref_x2s) and torch.equal(pool, ref_pool)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["relu_128_256_d2", "res_256_256_d2", "resb_256_512_d4", "relu_512_512_d4",
+                                  "fc_512_256_d1_ragged", "leaky_64_256_d1"])
+def test_conv3x3_matches_torch(case, device):
+    """pv_conv3x3_f16 (the wide 3x3 convolutions of layer3 / layer4 / fc with
+    their epilogue, RN:21-38 / MR:22-26) against MIOpen's fp16 convolution +
+    ATen's bias / residual / activation on the same inputs.  Both sum in f32
+    and round the convolution to fp16 (in other orders), so the outputs agree
+    within a couple of fp16 roundings of the convolution's scale; padding,
+    dilation and a pixel count that is not a multiple of the tile included."""
+    from pvnet_amd.network import conv3x3, conv3x3_weight
+    F = torch.nn.functional
+    kind, cin, cout, d = case.split("_")[0], *[int(v) for v in case.split("_")[1:3]], int(case.split("_")[3][1:])
+    n, h, w = (3, 13, 17) if case.endswith("ragged") else (2, 30, 40)
+    g = torch.Generator().manual_seed(cin * 7 + cout + d)
+    cl = torch.channels_last
+    x = torch.randn(n, cin, h, w, generator=g).to(device, torch.float16).contiguous(memory_format=cl)
+    conv = torch.nn.Conv2d(cin, cout, 3, 1, d, d, bias=True).to(device)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5))
+        conv.bias.copy_(torch.randn(cout, generator=g) * 0.5)
+    conv = conv.half()
+    res = torch.randn(n, cout, h, w, generator=g).to(device, torch.float16).contiguous(memory_format=cl)
+    rb = (torch.randn(cout, generator=g) * 0.5).to(device, torch.float16)
+    use_res, use_rb = kind in ("res", "resb"), kind == "resb"
+    act = "leaky" if kind == "leaky" else "relu"
+    with torch.no_grad():
+        y = F.conv2d(x, conv.weight, None, 1, d, d) + conv.bias.view(1, -1, 1, 1)
+        if use_res:
+            y = y + ((res + rb.view(1, -1, 1, 1)) if use_rb else res)
+        ref = F.leaky_relu(y, 0.1) if act == "leaky" else torch.relu(y)
+        got = conv3x3(x, conv3x3_weight(conv), conv.bias, d, act, res=res if use_res else None,
+                      rbias=rb if use_rb else None)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape and got.is_contiguous(memory_format=cl)
+    sc = float(ref.abs().max())
+    dev_ = (got.float() - ref.float()).abs()
+    print(f"conv3x3 {case}: max dev {float(dev_.max()):.3e}, mean {float(dev_.mean()):.2e} (scale {sc:.2f})")
+    assert float(dev_.max()) <= 2 ** -8 * sc
+    assert float(dev_.mean()) <= 2 ** -13 * sc

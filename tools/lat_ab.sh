@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 for rep in 1 2; do
   for v in "$@"; do
     PVVOTE_LIB=variants/$v.so timeout -k 10 120 python3 tools/lat_trace.py 20 > gpurun_out/lab_$v.$rep.log 2>&1 || exit $?
-    PVVOTE_LIB=variants/$v.so timeout -k 10 200 python3 bench.py --steps 30 --warmup 5 --skip-cpu --skip-e2e --skip-u1 > gpurun_out/labb_$v.$rep.log 2>&1 || exit $?
+    PVVOTE_LIB=variants/$v.so timeout -k 10 200 python3 bench.py --steps 30 --warmup 5 --skip-cpu --skip-e2e --skip-u1 --skip-config3 > gpurun_out/labb_$v.$rep.log 2>&1 || exit $?
     python3 - "$v" "$rep" <<'PY'
 import json, sys
 v, rep = sys.argv[1:]
