@@ -60,6 +60,9 @@ def build(force: bool = False, extra=()) -> str:
     if force or needs_build():
         cmd = [hipcc(), *HIPCC_FLAGS, *extra, "-o", OUT + ".tmp", *SRCS]
         subprocess.check_call(cmd)
+        # every reference resolved (an unresolved kernel stub only shows at load time)
+        import ctypes
+        ctypes.CDLL(os.path.abspath(OUT + ".tmp"), mode=ctypes.RTLD_LOCAL | os.RTLD_NOW)
         os.replace(OUT + ".tmp", OUT)
     return OUT
 

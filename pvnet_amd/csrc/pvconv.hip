@@ -409,7 +409,6 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 
 constexpr int kCT = 256;                   // couts per tile
 constexpr int kPT = 256;                   // pixels per tile
-constexpr int kStage = (kCT + kPT) * 128;  // bytes per stage (A then B), 64 KiB
 
 struct ConvArgs {
     const _Float16 *x;      // [N][H][W][Cin]
@@ -423,14 +422,27 @@ struct ConvArgs {
     int64_t M;              // pixels
 };
 
+// LDS image of a stage: row r's 16-byte segment s at granule 8 r + (s ^ (r & 7))
+__device__ __forceinline__ int conv_granule(int row, int seg) { return row * 8 + (seg ^ (row & 7)); }
+
+// 16 bytes a lane from a buffer straight to LDS (wave-uniform LDS base + 16 x lane)
+__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_base, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)lds_base, 16, voff, soff, 0,
+                                             0);
+}
+
 __global__ __launch_bounds__(512) void k_conv3x3(ConvArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kStage];
+    constexpr int KB = 64;                                 // K-step: one tap x 64 input channels
+    constexpr int RB = KB * 2;                             // bytes per LDS row
+    constexpr int STAGE = (kCT + kPT) * RB;                // 64 KiB
+    constexpr int GPR = RB / 16;                           // 16-byte granules per row
+    constexpr int NI = (kCT * RB) / (1024 * 8);            // buffer-to-LDS loads per wave per operand per stage
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STAGE];
     const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
     // XCD-aware tile order: blocks i, i + 8, ... share an XCD; give each XCD a
-    // contiguous range of tiles, cout tile major -- an XCD then streams one
-    // cout tile's weights (2.4 MB at Cin 512) through its 4 MiB L2
+    // contiguous range of tiles, cout tile major
     int bid = (int)blockIdx.x;
-{
+    {
         const int nb = (int)gridDim.x, q = nb / 8, r = nb % 8, x = bid % 8;
         bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
     }
@@ -442,13 +454,16 @@ __global__ __launch_bounds__(512) void k_conv3x3(ConvArgs a) {
     const __amdgpu_buffer_rsrc_t xr =
         __builtin_amdgcn_make_buffer_rsrc((void *)a.x, 0, (int)(a.M * a.Cin * 2), 0x00020000);
     const int K2 = 9 * a.Cin * 2;            // bytes per weight row
-    // this lane's 4 weight and 4 pixel granules per stage: granule g = (4 wid + i) 64 + lane
-    int woff[4], py[4], px[4];
-    int64_t pbase[4];
-    bool pin[4];
+    const int cbk = a.Cin / KB;              // channel blocks per tap
+    const int ksteps = 9 * cbk;
+    // this lane's NI weight and NI pixel granules per stage: granule g = (NI wid + i) 64 + lane
+    int woff[NI], py[NI], px[NI];
+    int64_t pbase[NI];
+    bool pin[NI];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int g = (4 * wid + i) * 64 + lane, row = g >> 3, seg = (g & 7) ^ (row & 7);
+    for (int i = 0; i < NI; ++i) {
+        const int g = (NI * wid + i) * 64 + lane, row = g / GPR, pseg = g % GPR;
+        const int seg = conv_granule(row, pseg) - row * GPR;   // the swizzle is an involution per row
         woff[i] = (n0 + row) * K2 + seg * 16;
         const int64_t p = p0 + row;
         pin[i] = p < a.M;
@@ -459,22 +474,18 @@ __global__ __launch_bounds__(512) void k_conv3x3(ConvArgs a) {
         pbase[i] = pc * a.Cin * 2 + seg * 16;
     }
     auto issue = [&](int s, int buf) {
-        const int tap = s / a.cblocks, cb = s - tap * a.cblocks;
+        const int tap = s / cbk, cb = s - tap * cbk;
         const int dy = (tap / 3 - 1) * a.dil, dx = (tap % 3 - 1) * a.dil;
-        uint8_t *st = lds + buf * kStage;
+        uint8_t *st = lds + buf * STAGE;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                wr, (__attribute__((address_space(3))) void *)(st + (4 * wid + i) * 1024), 16, woff[i],
-                (tap * a.Cin + cb * 64) * 2, 0, 0);
-        const int dpix = (dy * a.W + dx) * a.Cin * 2 + cb * 128;
+        for (int i = 0; i < NI; ++i)
+            glds16(wr, st + (NI * wid + i) * 1024, woff[i], (tap * a.Cin + cb * KB) * 2);
+        const int dpix = (dy * a.W + dx) * a.Cin * 2 + cb * RB;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < NI; ++i) {
             const bool ok = pin[i] && (unsigned)(py[i] + dy) < (unsigned)a.H && (unsigned)(px[i] + dx) < (unsigned)a.W;
             const uint32_t off = ok ? (uint32_t)(pbase[i] + dpix) : 0x80000000u;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                xr, (__attribute__((address_space(3))) void *)(st + kCT * 128 + (4 * wid + i) * 1024), 16, off, 0, 0,
-                0);
+            glds16(xr, st + kCT * RB + (NI * wid + i) * 1024, off, 0);
         }
     };
     const int wn = wid & 1, wm = wid >> 1;   // wave: couts wn*128 .. +127, pixels wm*64 .. +63
@@ -483,30 +494,20 @@ __global__ __launch_bounds__(512) void k_conv3x3(ConvArgs a) {
     for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f4v{0.f, 0.f, 0.f, 0.f};
-    issue(0, 0);
-    for (int s = 0; s < a.ksteps; ++s) {
-        const int buf = s & 1;
-        __builtin_amdgcn_s_waitcnt(0x0F70);          // this wave's loads of step s have landed (vmcnt 0)
-        __syncthreads();                              // ... and every wave's; step s-1's reads are done
-#ifdef PVC_NO_LOADS
-        if (s == 0 && a.ksteps > 1) issue(s + 1, buf ^ 1);
-#else
-        if (s + 1 < a.ksteps) issue(s + 1, buf ^ 1);
-#endif
-        const uint8_t *st = lds + buf * kStage;
+    auto compute = [&](const uint8_t *st) {
 #pragma unroll
-        for (int kc = 0; kc < 2; ++kc) {
+        for (int kc = 0; kc < KB / 32; ++kc) {
             const int sg = kc * 4 + (lane >> 4);
             h8v af[8], bf[4];
 #pragma unroll
             for (int mi = 0; mi < 8; ++mi) {
                 const int r = wn * 128 + mi * 16 + (lane & 15);
-                af[mi] = *(const h8v *)(st + (r * 8 + (sg ^ (r & 7))) * 16);
+                af[mi] = *(const h8v *)(st + conv_granule(r, sg) * 16);
             }
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni) {
                 const int r = wm * 64 + ni * 16 + (lane & 15);
-                bf[ni] = *(const h8v *)(st + kCT * 128 + (r * 8 + (sg ^ (r & 7))) * 16);
+                bf[ni] = *(const h8v *)(st + kCT * RB + conv_granule(r, sg) * 16);
             }
 #ifdef PVC_NO_MFMA
 #pragma unroll
@@ -519,6 +520,18 @@ __global__ __launch_bounds__(512) void k_conv3x3(ConvArgs a) {
                     acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mi], bf[ni], acc[mi][ni], 0, 0, 0);
 #endif
         }
+    };
+    issue(0, 0);
+    for (int s = 0; s < ksteps; ++s) {
+        const int buf = s & 1;
+        __builtin_amdgcn_s_waitcnt(0x0F70);          // this wave's loads of step s have landed (vmcnt 0)
+        __syncthreads();                              // ... and every wave's; step s-1's reads are done
+#ifdef PVC_NO_LOADS
+        if (s == 0 && ksteps > 1) issue(s + 1, buf ^ 1);
+#else
+        if (s + 1 < ksteps) issue(s + 1, buf ^ 1);
+#endif
+        compute(lds + buf * STAGE);
     }
     // ---- epilogue: lane's accumulator (mi, ni) = couts c .. c+3 of pixel p;
     // k_epilogue's roundings (bias add, residual (+ its bias), activation) ----
