@@ -392,8 +392,8 @@ unsigned long long *g_tail_trace = nullptr;
 // the conv epilogue (folded BN bias, residual, ReLU; k_epilogue's roundings)
 // fused.  D[cout][pixel] = sum_k W[cout][k] X[k][pixel], k = tap * Cin + c.
 //
-// Block: 8 waves, a 256-cout x 256-pixel tile (wave = 128 couts x 64 pixels:
-// 8 x 4 accumulator tiles of 16 x 16, 128 VGPRs).  K-step = 64 (one tap, 64
+// Block: 16 waves, a 256-cout x 256-pixel tile (wave = 64 couts x 64 pixels:
+// 4 x 4 accumulator tiles of 16 x 16; 111 VGPRs, 4 waves per SIMD).  K-step = 64 (one tap, 64
 // input channels): the weights' and the pixels' 256 rows x 128 bytes each go
 // to LDS by buffer loads straight to LDS (16 bytes a lane; rows outside the
 // image or past the map read as zeros -- the convolution's zero padding),
@@ -431,12 +431,19 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_ba
                                              0);
 }
 
-__global__ __launch_bounds__(512) void k_conv3x3(ConvArgs a) {
+#ifndef PVC_NW
+#define PVC_NW 16
+#endif
+constexpr int kNW = PVC_NW;                   // waves per block: 16 (4 cout x 4 pixel groups; 8 = 2 x 4 measured 5-8 % slower)
+
+__global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
     constexpr int KB = 64;                                 // K-step: one tap x 64 input channels
     constexpr int RB = KB * 2;                             // bytes per LDS row
     constexpr int STAGE = (kCT + kPT) * RB;                // 64 KiB
     constexpr int GPR = RB / 16;                           // 16-byte granules per row
-    constexpr int NI = (kCT * RB) / (1024 * 8);            // buffer-to-LDS loads per wave per operand per stage
+    constexpr int NI = (kCT * RB) / (1024 * kNW);          // buffer-to-LDS loads per wave per operand per stage
+    constexpr int WC = kNW / 4;                            // cout groups of waves
+    constexpr int MI = kCT / WC / 16;                      // 16-cout accumulator tiles per wave
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STAGE];
     const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
     // XCD-aware tile order: blocks i, i + 8, ... share an XCD; give each XCD a
@@ -488,20 +495,20 @@ __global__ __launch_bounds__(512) void k_conv3x3(ConvArgs a) {
             glds16(xr, st + kCT * RB + (NI * wid + i) * 1024, off, 0);
         }
     };
-    const int wn = wid & 1, wm = wid >> 1;   // wave: couts wn*128 .. +127, pixels wm*64 .. +63
-    f4v acc[8][4];
+    const int wn = wid % WC, wm = wid / WC;  // wave: couts wn*(256/WC) .., pixels wm*64 .. +63
+    f4v acc[MI][4];
 #pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f4v{0.f, 0.f, 0.f, 0.f};
     auto compute = [&](const uint8_t *st) {
 #pragma unroll
         for (int kc = 0; kc < KB / 32; ++kc) {
             const int sg = kc * 4 + (lane >> 4);
-            h8v af[8], bf[4];
+            h8v af[MI], bf[4];
 #pragma unroll
-            for (int mi = 0; mi < 8; ++mi) {
-                const int r = wn * 128 + mi * 16 + (lane & 15);
+            for (int mi = 0; mi < MI; ++mi) {
+                const int r = wn * (MI * 16) + mi * 16 + (lane & 15);
                 af[mi] = *(const h8v *)(st + conv_granule(r, sg) * 16);
             }
 #pragma unroll
@@ -511,10 +518,10 @@ __global__ __launch_bounds__(512) void k_conv3x3(ConvArgs a) {
             }
 #ifdef PVC_NO_MFMA
 #pragma unroll
-            for (int mi = 0; mi < 8; ++mi) acc[mi][0][0] += (float)af[mi][0] + (float)bf[mi & 3][1];
+            for (int mi = 0; mi < MI; ++mi) acc[mi][0][0] += (float)af[mi][0] + (float)bf[mi & 3][1];
 #else
 #pragma unroll
-            for (int mi = 0; mi < 8; ++mi)
+            for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
                 for (int ni = 0; ni < 4; ++ni)
                     acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mi], bf[ni], acc[mi][ni], 0, 0, 0);
@@ -535,10 +542,10 @@ __global__ __launch_bounds__(512) void k_conv3x3(ConvArgs a) {
     }
     // ---- epilogue: lane's accumulator (mi, ni) = couts c .. c+3 of pixel p;
     // k_epilogue's roundings (bias add, residual (+ its bias), activation) ----
-    h4 bq[8], rbq[8];
+    h4 bq[MI], rbq[MI];
 #pragma unroll
-    for (int mi = 0; mi < 8; ++mi) {
-        const int c = n0 + wn * 128 + mi * 16 + 4 * (lane >> 4);
+    for (int mi = 0; mi < MI; ++mi) {
+        const int c = n0 + wn * (MI * 16) + mi * 16 + 4 * (lane >> 4);
         bq[mi] = *(const h4 *)(a.bias + c);
         rbq[mi] = a.rbias ? *(const h4 *)(a.rbias + c) : h4{};
     }
@@ -547,15 +554,15 @@ __global__ __launch_bounds__(512) void k_conv3x3(ConvArgs a) {
         const int64_t p = p0 + wm * 64 + ni * 16 + (lane & 15);
         const bool pv = p < a.M;
         const int64_t pc = pv ? p : 0;
-        h4 r[8];
+        h4 r[MI];
         if (a.res) {
 #pragma unroll
-            for (int mi = 0; mi < 8; ++mi)
-                r[mi] = *(const h4 *)(a.res + pc * a.Cout + n0 + wn * 128 + mi * 16 + 4 * (lane >> 4));
+            for (int mi = 0; mi < MI; ++mi)
+                r[mi] = *(const h4 *)(a.res + pc * a.Cout + n0 + wn * (MI * 16) + mi * 16 + 4 * (lane >> 4));
         }
 #pragma unroll
-        for (int mi = 0; mi < 8; ++mi) {
-            const int c = n0 + wn * 128 + mi * 16 + 4 * (lane >> 4);
+        for (int mi = 0; mi < MI; ++mi) {
+            const int c = n0 + wn * (MI * 16) + mi * 16 + 4 * (lane >> 4);
             h4 y;
 #pragma unroll
             for (int j = 0; j < 4; ++j) y[j] = (_Float16)((float)(_Float16)acc[mi][ni][j] + (float)bq[mi][j]);
@@ -663,7 +670,7 @@ extern "C" int pv_conv3x3_f16(const void *x, const void *w, const void *bias, co
     a.ntp = (int)((a.M + kPT - 1) / kPT);
     a.nct = cout / kCT;
     a.ntiles = a.ntp * a.nct;
-    k_conv3x3<<<(unsigned)a.ntiles, 512, 0, (hipStream_t)stream>>>(a);
+    k_conv3x3<<<(unsigned)a.ntiles, 64 * kNW, 0, (hipStream_t)stream>>>(a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? PV_OK : (int)e;
 }
