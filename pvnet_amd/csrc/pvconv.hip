@@ -434,6 +434,9 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_ba
 #ifndef PVC_NW
 #define PVC_NW 16
 #endif
+#ifndef PVC_PRIO
+#define PVC_PRIO 0
+#endif
 constexpr int kNW = PVC_NW;                   // waves per block: 16 (4 cout x 4 pixel groups; 8 = 2 x 4 measured 5-8 % slower)
 
 __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
@@ -480,13 +483,17 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
         px[i] = rem - py[i] * a.W;
         pbase[i] = pc * a.Cin * 2 + seg * 16;
     }
-    auto issue = [&](int s, int buf) {
+    auto issue_w = [&](int s, int buf) {
         const int tap = s / cbk, cb = s - tap * cbk;
-        const int dy = (tap / 3 - 1) * a.dil, dx = (tap % 3 - 1) * a.dil;
         uint8_t *st = lds + buf * STAGE;
 #pragma unroll
         for (int i = 0; i < NI; ++i)
             glds16(wr, st + (NI * wid + i) * 1024, woff[i], (tap * a.Cin + cb * KB) * 2);
+    };
+    auto issue_x = [&](int s, int buf) {
+        const int tap = s / cbk, cb = s - tap * cbk;
+        const int dy = (tap / 3 - 1) * a.dil, dx = (tap % 3 - 1) * a.dil;
+        uint8_t *st = lds + buf * STAGE;
         const int dpix = (dy * a.W + dx) * a.Cin * 2 + cb * RB;
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
@@ -495,15 +502,16 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
             glds16(xr, st + kCT * RB + (NI * wid + i) * 1024, off, 0);
         }
     };
+    auto issue = [&](int s, int buf) { issue_w(s, buf); issue_x(s, buf); };
     const int wn = wid % WC, wm = wid / WC;  // wave: couts wn*(256/WC) .., pixels wm*64 .. +63
     f4v acc[MI][4];
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f4v{0.f, 0.f, 0.f, 0.f};
-    auto compute = [&](const uint8_t *st) {
-#pragma unroll
-        for (int kc = 0; kc < KB / 32; ++kc) {
+    // kc-th half of a step (32 of its 64 channels)
+    auto compute_kc = [&](const uint8_t *st, int kc) {
+        {
             const int sg = kc * 4 + (lane >> 4);
             h8v af[MI], bf[4];
 #pragma unroll
@@ -534,11 +542,27 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
         __builtin_amdgcn_s_waitcnt(0x0F70);          // this wave's loads of step s have landed (vmcnt 0)
         __syncthreads();                              // ... and every wave's; step s-1's reads are done
 #ifdef PVC_NO_LOADS
-        if (s == 0 && ksteps > 1) issue(s + 1, buf ^ 1);
+        const bool nx = s == 0 && ksteps > 1;
 #else
-        if (s + 1 < ksteps) issue(s + 1, buf ^ 1);
+        const bool nx = s + 1 < ksteps;
 #endif
-        compute(lds + buf * STAGE);
+#ifdef PVC_SPLIT
+        // the next step's weight loads, then half the MFMAs, then its pixel loads
+        if (nx) issue_w(s + 1, buf ^ 1);
+        if (PVC_PRIO) __builtin_amdgcn_s_setprio(1);
+        compute_kc(lds + buf * STAGE, 0);
+        if (PVC_PRIO) __builtin_amdgcn_s_setprio(0);
+        if (nx) issue_x(s + 1, buf ^ 1);
+        if (PVC_PRIO) __builtin_amdgcn_s_setprio(1);
+        compute_kc(lds + buf * STAGE, 1);
+        if (PVC_PRIO) __builtin_amdgcn_s_setprio(0);
+#else
+        if (nx) issue(s + 1, buf ^ 1);
+        if (PVC_PRIO) __builtin_amdgcn_s_setprio(1);
+        compute_kc(lds + buf * STAGE, 0);
+        compute_kc(lds + buf * STAGE, 1);
+        if (PVC_PRIO) __builtin_amdgcn_s_setprio(0);
+#endif
     }
     // ---- epilogue: lane's accumulator (mi, ni) = couts c .. c+3 of pixel p;
     // k_epilogue's roundings (bias add, residual (+ its bias), activation) ----
