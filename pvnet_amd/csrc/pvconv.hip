@@ -434,9 +434,6 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_ba
 #ifndef PVC_NW
 #define PVC_NW 16
 #endif
-#ifndef PVC_PRIO
-#define PVC_PRIO 0
-#endif
 constexpr int kNW = PVC_NW;                   // waves per block: 16 (4 cout x 4 pixel groups; 8 = 2 x 4 measured 5-8 % slower)
 
 __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
@@ -546,23 +543,9 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
 #else
         const bool nx = s + 1 < ksteps;
 #endif
-#ifdef PVC_SPLIT
-        // the next step's weight loads, then half the MFMAs, then its pixel loads
-        if (nx) issue_w(s + 1, buf ^ 1);
-        if (PVC_PRIO) __builtin_amdgcn_s_setprio(1);
-        compute_kc(lds + buf * STAGE, 0);
-        if (PVC_PRIO) __builtin_amdgcn_s_setprio(0);
-        if (nx) issue_x(s + 1, buf ^ 1);
-        if (PVC_PRIO) __builtin_amdgcn_s_setprio(1);
-        compute_kc(lds + buf * STAGE, 1);
-        if (PVC_PRIO) __builtin_amdgcn_s_setprio(0);
-#else
         if (nx) issue(s + 1, buf ^ 1);
-        if (PVC_PRIO) __builtin_amdgcn_s_setprio(1);
         compute_kc(lds + buf * STAGE, 0);
         compute_kc(lds + buf * STAGE, 1);
-        if (PVC_PRIO) __builtin_amdgcn_s_setprio(0);
-#endif
     }
     // ---- epilogue: lane's accumulator (mi, ni) = couts c .. c+3 of pixel p;
     // k_epilogue's roundings (bias add, residual (+ its bias), activation) ----
