@@ -266,6 +266,16 @@ int pv_conv3x3_f16(const void *x, const void *w, const void *bias, const void *r
                    int32_t ldo, int32_t n, int32_t h, int32_t wd, int32_t cin, int32_t cout, int32_t dil,
                    int32_t act, float slope, pv_stream_t stream);
 
+/* replaces the decoder's half-resolution step (model_repository.py:43-51,75-78: up4sto2s, torch.cat([fm,
+ * x2s], 1), conv2s = 3x3 conv + BN + LeakyReLU(slope)) in one fp16 matrix-core pass: fm [n][hin][win][64]
+ * (conv4s's output), skip [n][2hin][2win][64] (x2s), out [n][2hin][2win][32], all channels-last.  w: the
+ * 3x3 weights with BN folded, laid out [2][9][8][32][8] fp16: element [p][3 ky + kx][q][cout][j] =
+ * W[cout][64 p + 8 q + j][ky][kx] (p = 0 the upsampled channels, 1 the skip); bias fp16 [32].  fm, skip,
+ * w, out 16-byte, bias 8-byte aligned.  Roundings as pv_decoder_tail_f16's blend and convolution, then
+ * the bias add and LeakyReLU as ATen. */
+int pv_decoder_conv2s_f16(const void *fm, const void *skip, const void *w, const void *bias, void *out, int32_t n,
+                          int32_t hin, int32_t win, float slope, pv_stream_t stream);
+
 /* replaces the decoder's full-resolution tail (model_repository.py:75-79: up2storaw, torch.cat([fm, x], 1),
  * convraw = 3x3 conv + BN + LeakyReLU(slope) + 1x1 conv) in one fp16 pass on the matrix cores:
  * fm [n][hin][win][32] (conv2s's output, channels-last), img [n][2hin][2win][3] (the input batch,

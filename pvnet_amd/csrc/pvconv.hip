@@ -594,6 +594,207 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
     }
 }
 
+
+// ==========================================================================
+// conv2s with the upsampling and concatenation before it (MR:43-51,75-78:
+// up4sto2s, torch.cat([fm, x2s], 1), conv2s = 3x3 conv + BN + LeakyReLU):
+// out = leaky(conv3x3(cat(up2(fm), skip)) + b), fp16, channels-last, in one
+// pass: fm [N][Hin][Win][64] (conv4s's output), skip [N][H][W][64] (x2s),
+// out [N][H][W][32].  The unfused form writes the 128-channel cat (629 MB
+// at batch 32), reads it back nine times over for MIOpen's convolution and
+// passes its output through an epilogue.
+//
+// Persistent blocks of 8 waves (one per CU: 144 KiB LDS); an 8 x 32 output
+// tile; per tile the 10 x 34 halo is built twice in one LDS buffer -- first
+// the 64 upsampled channels (separable blend from a 7 x 19 fm patch, packed
+// fp16, as pv_decoder_tail), then the 64 skip channels (copied) -- and each
+// time every wave runs its 32-pixel output row's half of the convolution:
+// 36 v_mfma_f32_32x32x16_f16, A = the weights (all 73.7 KB of them resident
+// in LDS for the launch, read as one 16-byte row fragment per MFMA), B = one
+// 16-byte LDS read of 8 channels of one halo pixel (XOR-swizzled within the
+// pixel's 128 bytes: conflict-free).  The next tile's patch and skip pixels
+// are loaded into registers (buffer loads, zero outside the maps) while this
+// tile convolves.  Epilogue in registers: fp16 round of the f32 sums, + b,
+// LeakyReLU (y * slope in f32), 8-byte stores of 4 consecutive channels.
+// ==========================================================================
+constexpr int kDCo = 32, kDC1 = 64, kDC2 = 64;
+constexpr int kDOct = 9 * (kDC1 + kDC2) / 8;          // weight octets (16 bytes of 8 channels): 144
+constexpr int kDPatch = kPR * kPC * (kDC1 / 8);       // fm patch chunks: 1064
+constexpr int kDPatchIt = (kDPatch + 511) / 512;
+constexpr int kDTcol = kPR * kHC * (kDC1 / 8);        // column blends: 1904
+constexpr int kDHalo = kHaloPx * 8;                   // halo chunks per part: 2720
+constexpr int kDSkipIt = (kDHalo + 511) / 512;
+
+struct DecConvArgs {
+    const _Float16 *fm, *skip;
+    const _Float16 *w;      // [2 parts][9 taps][8 octets][32 couts][8]: the LDS image of the weights
+    const _Float16 *bias;   // [32]
+    _Float16 *out;
+    int N, Hin, Win, H, W, tiles_r, tiles_c, ntiles;
+    float rh, rw, slope;
+};
+
+__device__ __forceinline__ int halo_granule(int hp, int q) { return hp * 8 + (q ^ (hp & 7)); }
+
+__global__ __launch_bounds__(512) void k_dec_conv2s(DecConvArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kDOct * kDCo * 16 + kDHalo * 16 + kDTcol * 16];
+    uint8_t *wl = lds;                                  // 73,728 B
+    uint8_t *halo = lds + kDOct * kDCo * 16;            // 43,520 B (the fm patch aliases its front)
+    uint8_t *tcol = halo + kDHalo * 16;                 // 30,464 B
+    const int t = (int)threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int n = lane & 31, h = lane >> 5;
+    // the weights, once per launch
+    for (int i = t; i < kDOct * kDCo; i += 512) *(h8 *)(wl + i * 16) = *(const h8 *)(a.w + i * 8);
+    const h4 bq[4] = {*(const h4 *)(a.bias + 0 + 4 * h), *(const h4 *)(a.bias + 8 + 4 * h),
+                      *(const h4 *)(a.bias + 16 + 4 * h), *(const h4 *)(a.bias + 24 + 4 * h)};
+    auto coords = [&](int tile, int &b, int &y0, int &x0, int &ly0, int &lx0) {
+        const int tc = tile % a.tiles_c, rest = tile / a.tiles_c;
+        b = rest / a.tiles_r;
+        y0 = (rest % a.tiles_r) * kTR;
+        x0 = tc * kTC;
+        ly0 = (int)(a.rh * (float)max(y0 - 1, 0));
+        lx0 = (int)(a.rw * (float)max(x0 - 1, 0));
+    };
+    // prefetch of a tile's fm patch and skip halo into registers
+    h8 ppre[kDPatchIt], spre[kDSkipIt];
+    auto fetch = [&](int tile) {
+        int b, y0, x0, ly0, lx0;
+        coords(tile, b, y0, x0, ly0, lx0);
+        const __amdgpu_buffer_rsrc_t fr = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(a.fm + (int64_t)b * a.Hin * a.Win * kDC1), 0, a.Hin * a.Win * kDC1 * 2, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < kDPatchIt; ++i) {
+            const int c = min(t + 512 * i, kDPatch - 1), pp = c >> 3, q = c & 7;
+            const int pr = pp / kPC, pc = pp - pr * kPC;
+            const int off = ((ly0 + pr) * a.Win + lx0 + pc) * (kDC1 * 2) + q * 16;   // rows past fm read 0
+            ppre[i] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(fr, off, 0, 0));
+        }
+        const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(a.skip + (int64_t)b * a.H * a.W * kDC2), 0, a.H * a.W * kDC2 * 2, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < kDSkipIt; ++i) {
+            const int c = min(t + 512 * i, kDHalo - 1), hp = c >> 3, q = c & 7;
+            const int hy = hp / kHC, hx = hp - hy * kHC;
+            const int oy = y0 - 1 + hy, ox = x0 - 1 + hx;
+            const bool ok = oy >= 0 && oy < a.H && ox >= 0 && ox < a.W;
+            const uint32_t off = ok ? (uint32_t)((oy * a.W + ox) * (kDC2 * 2) + q * 16) : 0x80000000u;
+            spre[i] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(sr, off, 0, 0));
+        }
+    };
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    int tile = (int)blockIdx.x;
+    if (tile < a.ntiles) fetch(tile);
+    for (; tile < a.ntiles; tile += (int)gridDim.x) {
+        int b, y0, x0, ly0, lx0;
+        coords(tile, b, y0, x0, ly0, lx0);
+        __syncthreads();                      // the previous tile's skip-part reads of the halo are done
+#pragma unroll
+        for (int i = 0; i < kDPatchIt; ++i)
+            if (t + 512 * i < kDPatch) *(h8 *)(halo + (t + 512 * i) * 16) = ppre[i];   // patch, at the halo's front
+        __syncthreads();
+        // column blends: (fm row r, halo column hx, octet q) -> tcol [r][hx][q]
+        for (int task = t; task < kDTcol; task += 512) {
+            const int q = task & 7, rc = task >> 3;
+            const int r = rc / kHC, hx = rc - r * kHC;
+            const int ox = min(max(x0 - 1 + hx, 0), a.W - 1);
+            const float w1r = a.rw * (float)ox;
+            const int w1 = (int)w1r, w1p = w1 < a.Win - 1 ? 8 : 0;
+            const float w1l = w1r - (float)w1;
+            const uint8_t *pp = halo + ((r * kPC + (w1 - lx0)) * 8 + q) * 16;
+            const h8 A = *(const h8 *)pp, B = *(const h8 *)(pp + w1p * 16);
+            *(h8 *)(tcol + task * 16) =
+                __builtin_elementwise_fma(B, (h8)(_Float16)w1l, A * (h8)(_Float16)(1.f - w1l));
+        }
+        __syncthreads();                      // the patch is dead: the halo may be written
+        // row blends -> halo (upsampled channels, zero outside the image)
+        for (int task = t; task < kDHalo; task += 512) {
+            const int q = task & 7, hp = task >> 3;
+            const int hy = hp / kHC, hx = hp - hy * kHC;
+            const int oy = y0 - 1 + hy, ox = x0 - 1 + hx;
+            h8 v = {};
+            if (oy >= 0 && oy < a.H && ox >= 0 && ox < a.W) {
+                const float h1r = a.rh * (float)oy;
+                const int h1 = (int)h1r;
+                const int dh = h1 < a.Hin - 1 ? kHC * 8 * 16 : 0;
+                const float h1l = h1r - (float)h1;
+                const uint8_t *tp = tcol + (((h1 - ly0) * kHC + hx) * 8 + q) * 16;
+                const h8 c0 = *(const h8 *)tp, c1 = *(const h8 *)(tp + dh);
+                v = __builtin_elementwise_fma(c1, (h8)(_Float16)h1l, c0 * (h8)(_Float16)(1.f - h1l));
+            }
+            *(h8 *)(halo + halo_granule(hp, q) * 16) = v;
+        }
+        __syncthreads();
+        if (tile + (int)gridDim.x < a.ntiles) {
+            // the next tile's patch now (its skip pixels are still needed below)
+            int nb, ny0, nx0, nly0, nlx0;
+            coords(tile + (int)gridDim.x, nb, ny0, nx0, nly0, nlx0);
+            const __amdgpu_buffer_rsrc_t fr = __builtin_amdgcn_make_buffer_rsrc(
+                (void *)(a.fm + (int64_t)nb * a.Hin * a.Win * kDC1), 0, a.Hin * a.Win * kDC1 * 2, 0x00020000);
+#pragma unroll
+            for (int i = 0; i < kDPatchIt; ++i) {
+                const int c = min(t + 512 * i, kDPatch - 1), pp = c >> 3, q = c & 7;
+                const int pr = pp / kPC, pc = pp - pr * kPC;
+                const int off = ((nly0 + pr) * a.Win + nlx0 + pc) * (kDC1 * 2) + q * 16;
+                ppre[i] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(fr, off, 0, 0));
+            }
+        }
+        // ---- the convolution, part by part: wave = output row wid, 32 pixels ----
+        f16x acc = {};
+        auto conv_part = [&](int part) {
+#pragma unroll 4
+            for (int s = 0; s < 36; ++s) {
+                const int o = 2 * s + h;                  // octet of this lane half: tap o / 8, channels 8 (o % 8)
+                const int tap = o >> 3, q = o & 7;
+                const int ky = tap / 3, kx = tap - 3 * ky;
+                const h8 af = *(const h8 *)(wl + ((part * 72 + o) * kDCo + n) * 16);
+                const int hp = (wid + ky) * kHC + n + kx;
+                const h8 bf = *(const h8 *)(halo + halo_granule(hp, q) * 16);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc, 0, 0, 0);
+            }
+        };
+        conv_part(0);
+        __syncthreads();                      // every wave is done with the upsampled halo
+#pragma unroll
+        for (int i = 0; i < kDSkipIt; ++i) {
+            const int c = t + 512 * i;
+            if (c < kDHalo) *(h8 *)(halo + halo_granule(c >> 3, c & 7) * 16) = spre[i];
+        }
+        __syncthreads();
+        if (tile + (int)gridDim.x < a.ntiles) {
+            int nb, ny0, nx0, nly0, nlx0;
+            coords(tile + (int)gridDim.x, nb, ny0, nx0, nly0, nlx0);
+            const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
+                (void *)(a.skip + (int64_t)nb * a.H * a.W * kDC2), 0, a.H * a.W * kDC2 * 2, 0x00020000);
+#pragma unroll
+            for (int i = 0; i < kDSkipIt; ++i) {
+                const int c = min(t + 512 * i, kDHalo - 1), hp = c >> 3, q = c & 7;
+                const int hy = hp / kHC, hx = hp - hy * kHC;
+                const int oy = ny0 - 1 + hy, ox = nx0 - 1 + hx;
+                const bool ok = oy >= 0 && oy < a.H && ox >= 0 && ox < a.W;
+                const uint32_t off = ok ? (uint32_t)((oy * a.W + ox) * (kDC2 * 2) + q * 16) : 0x80000000u;
+                spre[i] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(sr, off, 0, 0));
+            }
+        }
+        conv_part(1);
+        // ---- epilogue: rows (i & 3) + 8 (i >> 2) + 4 h of acc = couts, column n = pixel ----
+        const int oy = y0 + wid, ox = x0 + n;
+        if (oy < a.H && ox < a.W) {
+            _Float16 *op = a.out + (((int64_t)b * a.H + oy) * a.W + ox) * kDCo;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                h4 y;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) y[j] = (_Float16)acc[4 * g + j];
+                y = y + bq[g];
+                h4 ys;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) ys[j] = (_Float16)((float)y[j] * a.slope);
+                *(h4 *)(op + 8 * g + 4 * h) = __builtin_elementwise_max(y, ys);
+            }
+        }
+    }
+}
+
 int cu_count_dec() {
     static int n = 0;
     if (!n) {
@@ -678,6 +879,32 @@ extern "C" int pv_conv3x3_f16(const void *x, const void *w, const void *bias, co
     a.nct = cout / kCT;
     a.ntiles = a.ntp * a.nct;
     k_conv3x3<<<(unsigned)a.ntiles, 64 * kNW, 0, (hipStream_t)stream>>>(a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? PV_OK : (int)e;
+}
+
+extern "C" int pv_decoder_conv2s_f16(const void *fm, const void *skip, const void *w, const void *bias, void *out,
+                                     int32_t n, int32_t hin, int32_t win, float slope, pv_stream_t stream) {
+    if (!fm || !skip || !w || !bias || !out || n < 0 || hin < 2 || win < 2) return PV_EINVAL;
+    if (!(slope >= 0.f && slope < 1.f)) return PV_EINVAL;
+    if (((uintptr_t)fm | (uintptr_t)skip | (uintptr_t)w | (uintptr_t)out) % 16 || (uintptr_t)bias % 8)
+        return PV_EALIGN;
+    if (n == 0) return PV_OK;
+    DecConvArgs a;
+    a.fm = (const _Float16 *)fm; a.skip = (const _Float16 *)skip; a.w = (const _Float16 *)w;
+    a.bias = (const _Float16 *)bias; a.out = (_Float16 *)out;
+    a.N = n; a.Hin = hin; a.Win = win; a.H = 2 * hin; a.W = 2 * win;
+    if ((int64_t)a.H * a.W * kDC2 * 2 >= (1ll << 31) || (int64_t)hin * win * kDC1 * 2 >= (1ll << 31)) return PV_EINVAL;
+    a.tiles_r = (a.H + kTR - 1) / kTR;
+    a.tiles_c = (a.W + kTC - 1) / kTC;
+    const int64_t nt = (int64_t)n * a.tiles_r * a.tiles_c;
+    if (nt >= (1ll << 31)) return PV_EINVAL;
+    a.ntiles = (int)nt;
+    a.rh = (float)(hin - 1) / (float)(a.H - 1);
+    a.rw = (float)(win - 1) / (float)(a.W - 1);
+    a.slope = slope;
+    const int64_t grid = std::min<int64_t>(nt, cu_count_dec());   // persistent: one block per CU
+    k_dec_conv2s<<<(unsigned)grid, 512, 0, (hipStream_t)stream>>>(a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? PV_OK : (int)e;
 }

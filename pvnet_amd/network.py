@@ -298,6 +298,36 @@ def conv3x3_weight(c: nn.Conv2d) -> torch.Tensor:
     return c.weight.detach().permute(0, 2, 3, 1).contiguous().half()
 
 
+def decoder_conv2s_weights(c: nn.Conv2d):
+    """conv2s's 3x3 weights (BN folded, 128 -> 32) in ``pv_decoder_conv2s_f16``'s
+    layout [2][9][8][32][8] fp16 and its bias (fp16)."""
+    if c.kernel_size != (3, 3) or c.in_channels != 128 or c.out_channels != 32 or c.padding != (1, 1):
+        raise RuntimeError("decoder_conv2s: conv2s must be a 3x3, 128 -> 32, padding-1 convolution")
+    w = c.weight.detach().float()                                   # [32, 128, 3, 3]
+    w = w.reshape(32, 2, 8, 8, 3, 3).permute(1, 4, 5, 2, 0, 3)      # [part, ky, kx, q, cout, j]
+    return w.reshape(2, 9, 8, 32, 8).contiguous().half(), c.bias.detach().half().contiguous()
+
+
+def decoder_conv2s(fm: torch.Tensor, skip: torch.Tensor, weights, slope: float = 0.1) -> torch.Tensor:
+    """up4sto2s + torch.cat([fm, x2s], 1) + conv2s (MR:43-51) in one fp16
+    matrix-core pass (``pv_decoder_conv2s_f16``): fm [n, 64, h, w] and skip
+    [n, 64, 2h, 2w] channels_last float16 CUDA; ``weights`` from
+    :func:`decoder_conv2s_weights`.  Returns [n, 32, 2h, 2w] channels_last."""
+    n, c, h, w = fm.shape
+    cl = torch.channels_last
+    if fm.dtype != torch.float16 or skip.dtype != torch.float16 or not fm.is_cuda:
+        raise RuntimeError("decoder_conv2s: float16 CUDA maps required")
+    if c != 64 or tuple(skip.shape) != (n, 64, 2 * h, 2 * w):
+        raise RuntimeError("decoder_conv2s: fm [n, 64, h, w] and skip [n, 64, 2h, 2w] required")
+    if not fm.is_contiguous(memory_format=cl) or not skip.is_contiguous(memory_format=cl):
+        raise RuntimeError("decoder_conv2s: channels_last maps required")
+    wt, b = weights
+    out = torch.empty((n, 32, 2 * h, 2 * w), dtype=fm.dtype, device=fm.device, memory_format=cl)
+    _dev_call("pv_decoder_conv2s_f16", None, fm, fm.data_ptr(), skip.data_ptr(), wt.data_ptr(), b.data_ptr(),
+              out.data_ptr(), n, h, w, float(slope))
+    return out
+
+
 def decoder_tail_weights(c0: nn.Conv2d, c1: nn.Conv2d, cin: int = 35):
     """convraw's weights (MR:53-58, BN folded into ``c0``) laid out for
     ``pv_decoder_tail_f16`` (include/pvvote.h): w1 [32][368] fp16 with
@@ -451,8 +481,17 @@ class PVNetInference(nn.Module):
         fm = conv_epilogue(_conv(cat8, self.conv8s[0]), self.conv8s[0].bias, "leaky")
         fm = upsample2x_cat(fm, x4s, fm.shape[1] + x4s.shape[1])
         fm = conv_epilogue(_conv(fm, self.conv4s[0]), self.conv4s[0].bias, "leaky")
-        fm = upsample2x_cat(fm, x2s, fm.shape[1] + x2s.shape[1])
-        fm = conv_epilogue(_conv(fm, self.conv2s[0]), self.conv2s[0].bias, "leaky")
+        c2 = self.conv2s[0]
+        if (fm.dtype == torch.float16 and self.fused_conv and fm.shape[1] == 64 and x2s.shape[1] == 64
+                and c2.in_channels == 128 and c2.out_channels == 32 and c2.kernel_size == (3, 3)):
+            key = (c2.weight.data_ptr(), c2.weight._version, c2.bias.data_ptr())
+            if getattr(self, "_c2s_key", None) != key:     # the kernel's weight layout, made once
+                self._c2s_w = decoder_conv2s_weights(c2)
+                self._c2s_key = key
+            fm = decoder_conv2s(fm, x2s, self._c2s_w, self.conv2s[2].negative_slope)
+        else:
+            fm = upsample2x_cat(fm, x2s, fm.shape[1] + x2s.shape[1])
+            fm = conv_epilogue(_conv(fm, c2), c2.bias, "leaky")
         c0, c1 = self.convraw[0], self.convraw[3]
         slope = self.convraw[2].negative_slope
         if x.dtype == torch.float16 and self.fused_tail:

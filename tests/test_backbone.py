@@ -525,3 +525,38 @@ def test_conv3x3_matches_torch(case, device):
     print(f"conv3x3 {case}: max dev {float(dev_.max()):.3e}, mean {float(dev_.mean()):.2e} (scale {sc:.2f})")
     assert float(dev_.max()) <= 2 ** -8 * sc
     assert float(dev_.mean()) <= 2 ** -13 * sc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hw", [(13, 21), (60, 80)])
+def test_decoder_conv2s_matches_torch(hw, device):
+    """pv_decoder_conv2s_f16 (up4sto2s + cat([fm, x2s]) + conv2s, MR:43-51, one
+    matrix-core pass) against ATen's unfused fp16 ops on the same inputs:
+    F.interpolate + torch.cat + the 3x3 conv + bias + LeakyReLU.  The blend's
+    fp16 weights and the summation order differ, so the outputs agree within
+    a couple of fp16 roundings of the convolution's scale; ragged tiles
+    (26 x 42) included."""
+    from pvnet_amd.network import decoder_conv2s, decoder_conv2s_weights
+    F = torch.nn.functional
+    g = torch.Generator().manual_seed(hw[0] * 31 + hw[1])
+    cl = torch.channels_last
+    n, (h, w) = 2, hw
+    fm = (torch.randn(n, 64, h, w, generator=g) * 2).to(device, torch.float16).contiguous(memory_format=cl)
+    skip = torch.randn(n, 64, 2 * h, 2 * w, generator=g).to(device, torch.float16).contiguous(memory_format=cl)
+    c = torch.nn.Conv2d(128, 32, 3, 1, 1).to(device)
+    with torch.no_grad():
+        c.weight.copy_(torch.randn(32, 128, 3, 3, generator=g) * 0.05)
+        c.bias.copy_(torch.randn(32, generator=g) * 0.5)
+    c = c.half()
+    with torch.no_grad():
+        up = F.interpolate(fm, scale_factor=2, mode="bilinear", align_corners=True)
+        y = F.conv2d(torch.cat([up, skip], 1), c.weight, None, 1, 1) + c.bias.view(1, -1, 1, 1)
+        ref = F.leaky_relu(y, 0.1)
+        got = decoder_conv2s(fm, skip, decoder_conv2s_weights(c), 0.1)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape and got.is_contiguous(memory_format=cl)
+    sc = float(ref.abs().max())
+    d = (got.float() - ref.float()).abs()
+    print(f"decoder conv2s {2 * h}x{2 * w}: max dev {float(d.max()):.3e}, mean {float(d.mean()):.2e} (scale {sc:.2f})")
+    assert float(d.max()) <= 2 ** -7 * sc
+    assert float(d.mean()) <= 2 ** -12 * sc
