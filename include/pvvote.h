@@ -276,6 +276,14 @@ int pv_conv3x3_f16(const void *x, const void *w, const void *bias, const void *r
 int pv_decoder_conv2s_f16(const void *fm, const void *skip, const void *w, const void *bias, void *out, int32_t n,
                           int32_t hin, int32_t win, float slope, pv_stream_t stream);
 
+/* replaces the decoder's quarter-resolution step (model_repository.py:35-43,75-77: up8sto4s, torch.cat([fm,
+ * x4s], 1), conv4s = 3x3 conv + BN + LeakyReLU) in one fp16 matrix-core pass: fm [n][hin][win][128]
+ * (conv8s's output), skip [n][2hin][2win][64] (x4s), out [n][2hin][2win][64].  w: [3][9][8][2][32][8] fp16,
+ * element [p][3 ky + kx][q][m][c][j] = W[32 m + c][64 p + 8 q + j][ky][kx] (p = 0, 1 the upsampled channels,
+ * 2 the skip); bias fp16 [64].  Alignment and roundings as pv_decoder_conv2s_f16. */
+int pv_decoder_conv4s_f16(const void *fm, const void *skip, const void *w, const void *bias, void *out, int32_t n,
+                          int32_t hin, int32_t win, float slope, pv_stream_t stream);
+
 /* replaces the decoder's full-resolution tail (model_repository.py:75-79: up2storaw, torch.cat([fm, x], 1),
  * convraw = 3x3 conv + BN + LeakyReLU(slope) + 1x1 conv) in one fp16 pass on the matrix cores:
  * fm [n][hin][win][32] (conv2s's output, channels-last), img [n][2hin][2win][3] (the input batch,

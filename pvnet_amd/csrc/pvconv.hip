@@ -795,6 +795,181 @@ __global__ __launch_bounds__(512) void k_dec_conv2s(DecConvArgs a) {
     }
 }
 
+
+// ==========================================================================
+// conv4s with the upsampling and concatenation before it (MR:35-43,75-77:
+// up8sto4s, torch.cat([fm, x4s], 1), conv4s = 3x3 conv + BN + LeakyReLU):
+// fm [N][Hin][Win][128] (conv8s's output), skip [N][H][W][64] (x4s), out
+// [N][H][W][64], fp16 channels-last, one pass.  k_dec_conv2s's structure
+// with 192 input channels in three 64-channel parts (upsampled 0..63,
+// upsampled 64..127, skip) and 64 output channels (two 32 x 32 accumulators
+// per wave); the 221 KB of weights do not fit in LDS beside the halo, so each
+// part's 73.7 KB are loaded straight to LDS (buffer loads) while its halo is
+// built.
+// ==========================================================================
+constexpr int kEC1 = 128, kECo = 64;
+constexpr int kEWPart = 9 * 8 * kECo;                 // weight octets (16 B) per part: 4608
+constexpr int kEWIt = kEWPart * 16 / (1024 * 8);      // buffer-to-LDS loads per wave per part: 9
+
+__global__ __launch_bounds__(512) void k_dec_conv4s(DecConvArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kEWPart * 16 + kDHalo * 16 + kDTcol * 16];
+    uint8_t *wl = lds;                                  // 73,728 B: this part's weights
+    uint8_t *halo = lds + kEWPart * 16;                 // 43,520 B (the fm patch aliases its front)
+    uint8_t *tcol = halo + kDHalo * 16;                 // 30,464 B
+    const int t = (int)threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int n = lane & 31, h = lane >> 5;
+    h4 bq[2][4];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) bq[m][g] = *(const h4 *)(a.bias + 32 * m + 8 * g + 4 * h);
+    const __amdgpu_buffer_rsrc_t wr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.w, 0, 3 * kEWPart * 16, 0x00020000);
+    auto load_w = [&](int part) {   // this part's LDS image, 1 KB per wave instruction
+#pragma unroll
+        for (int i = 0; i < kEWIt; ++i)
+            glds16(wr, wl + (kEWIt * wid + i) * 1024, (uint32_t)(((kEWIt * wid + i) * 64 + lane) * 16),
+                   (uint32_t)(part * kEWPart * 16));
+    };
+    auto coords = [&](int tile, int &b, int &y0, int &x0, int &ly0, int &lx0) {
+        const int tc = tile % a.tiles_c, rest = tile / a.tiles_c;
+        b = rest / a.tiles_r;
+        y0 = (rest % a.tiles_r) * kTR;
+        x0 = tc * kTC;
+        ly0 = (int)(a.rh * (float)max(y0 - 1, 0));
+        lx0 = (int)(a.rw * (float)max(x0 - 1, 0));
+    };
+    h8 ppre[kDPatchIt], spre[kDSkipIt];
+    // 64-channel slice `half` of a tile's fm patch
+    auto fetch_patch = [&](int tile, int half) {
+        int b, y0, x0, ly0, lx0;
+        coords(tile, b, y0, x0, ly0, lx0);
+        const __amdgpu_buffer_rsrc_t fr = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(a.fm + (int64_t)b * a.Hin * a.Win * kEC1), 0, a.Hin * a.Win * kEC1 * 2, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < kDPatchIt; ++i) {
+            const int c = min(t + 512 * i, kDPatch - 1), pp = c >> 3, q = c & 7;
+            const int pr = pp / kPC, pc = pp - pr * kPC;
+            const int off = ((ly0 + pr) * a.Win + lx0 + pc) * (kEC1 * 2) + half * 128 + q * 16;
+            ppre[i] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(fr, off, 0, 0));
+        }
+    };
+    auto fetch_skip = [&](int tile) {
+        int b, y0, x0, ly0, lx0;
+        coords(tile, b, y0, x0, ly0, lx0);
+        const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(a.skip + (int64_t)b * a.H * a.W * kDC2), 0, a.H * a.W * kDC2 * 2, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < kDSkipIt; ++i) {
+            const int c = min(t + 512 * i, kDHalo - 1), hp = c >> 3, q = c & 7;
+            const int hy = hp / kHC, hx = hp - hy * kHC;
+            const int oy = y0 - 1 + hy, ox = x0 - 1 + hx;
+            const bool ok = oy >= 0 && oy < a.H && ox >= 0 && ox < a.W;
+            const uint32_t off = ok ? (uint32_t)((oy * a.W + ox) * (kDC2 * 2) + q * 16) : 0x80000000u;
+            spre[i] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(sr, off, 0, 0));
+        }
+    };
+    // the upsampled halo of the patch in ppre (64 channels)
+    auto build_up = [&](int y0, int x0, int ly0, int lx0) {
+#pragma unroll
+        for (int i = 0; i < kDPatchIt; ++i)
+            if (t + 512 * i < kDPatch) *(h8 *)(halo + (t + 512 * i) * 16) = ppre[i];
+        __syncthreads();
+        for (int task = t; task < kDTcol; task += 512) {
+            const int q = task & 7, rc = task >> 3;
+            const int r = rc / kHC, hx = rc - r * kHC;
+            const int ox = min(max(x0 - 1 + hx, 0), a.W - 1);
+            const float w1r = a.rw * (float)ox;
+            const int w1 = (int)w1r, w1p = w1 < a.Win - 1 ? 8 : 0;
+            const float w1l = w1r - (float)w1;
+            const uint8_t *pp = halo + ((r * kPC + (w1 - lx0)) * 8 + q) * 16;
+            const h8 A = *(const h8 *)pp, B = *(const h8 *)(pp + w1p * 16);
+            *(h8 *)(tcol + task * 16) =
+                __builtin_elementwise_fma(B, (h8)(_Float16)w1l, A * (h8)(_Float16)(1.f - w1l));
+        }
+        __syncthreads();
+        for (int task = t; task < kDHalo; task += 512) {
+            const int q = task & 7, hp = task >> 3;
+            const int hy = hp / kHC, hx = hp - hy * kHC;
+            const int oy = y0 - 1 + hy, ox = x0 - 1 + hx;
+            h8 v = {};
+            if (oy >= 0 && oy < a.H && ox >= 0 && ox < a.W) {
+                const float h1r = a.rh * (float)oy;
+                const int h1 = (int)h1r;
+                const int dh = h1 < a.Hin - 1 ? kHC * 8 * 16 : 0;
+                const float h1l = h1r - (float)h1;
+                const uint8_t *tp = tcol + (((h1 - ly0) * kHC + hx) * 8 + q) * 16;
+                const h8 c0 = *(const h8 *)tp, c1 = *(const h8 *)(tp + dh);
+                v = __builtin_elementwise_fma(c1, (h8)(_Float16)h1l, c0 * (h8)(_Float16)(1.f - h1l));
+            }
+            *(h8 *)(halo + halo_granule(hp, q) * 16) = v;
+        }
+    };
+    f16x acc[2];
+    auto conv_part = [&]() {
+#pragma unroll 4
+        for (int s = 0; s < 36; ++s) {
+            const int o = 2 * s + h;
+            const int tap = o >> 3, q = o & 7;
+            const int ky = tap / 3, kx = tap - 3 * ky;
+            const int hp = (wid + ky) * kHC + n + kx;
+            const h8 bf = *(const h8 *)(halo + halo_granule(hp, q) * 16);
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const h8 af = *(const h8 *)(wl + ((o * 2 + m) * 32 + n) * 16);
+                acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[m], 0, 0, 0);
+            }
+        }
+    };
+    int tile = (int)blockIdx.x;
+    if (tile < a.ntiles) { fetch_patch(tile, 0); fetch_skip(tile); }
+    for (; tile < a.ntiles; tile += (int)gridDim.x) {
+        int b, y0, x0, ly0, lx0;
+        coords(tile, b, y0, x0, ly0, lx0);
+        const bool more = tile + (int)gridDim.x < a.ntiles;
+        acc[0] = acc[1] = f16x{};
+#pragma unroll 1
+        for (int part = 0; part < 3; ++part) {
+            __syncthreads();                  // the previous part's convolution is done with halo and weights
+            load_w(part);                     // lands while the halo is built
+            if (part < 2) {
+                build_up(y0, x0, ly0, lx0);
+            } else {
+#pragma unroll
+                for (int i = 0; i < kDSkipIt; ++i) {
+                    const int c = t + 512 * i;
+                    if (c < kDHalo) *(h8 *)(halo + halo_granule(c >> 3, c & 7) * 16) = spre[i];
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // this wave's weight loads have landed
+            __syncthreads();
+            // the next part's inputs, in flight during this part's convolution
+            if (part == 0) fetch_patch(tile, 1);
+            else if (part == 1 && more) fetch_patch(tile + (int)gridDim.x, 0);
+            else if (part == 2 && more) fetch_skip(tile + (int)gridDim.x);
+            conv_part();
+        }
+        // ---- epilogue: acc[m] rows (i & 3) + 8 (i >> 2) + 4 h = couts 32 m + .., column n = pixel ----
+        const int oy = y0 + wid, ox = x0 + n;
+        if (oy < a.H && ox < a.W) {
+            _Float16 *op = a.out + (((int64_t)b * a.H + oy) * a.W + ox) * kECo;
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    h4 y;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) y[j] = (_Float16)acc[m][4 * g + j];
+                    y = y + bq[m][g];
+                    h4 ys;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) ys[j] = (_Float16)((float)y[j] * a.slope);
+                    *(h4 *)(op + 32 * m + 8 * g + 4 * h) = __builtin_elementwise_max(y, ys);
+                }
+        }
+    }
+}
+
 int cu_count_dec() {
     static int n = 0;
     if (!n) {
@@ -905,6 +1080,32 @@ extern "C" int pv_decoder_conv2s_f16(const void *fm, const void *skip, const voi
     a.slope = slope;
     const int64_t grid = std::min<int64_t>(nt, cu_count_dec());   // persistent: one block per CU
     k_dec_conv2s<<<(unsigned)grid, 512, 0, (hipStream_t)stream>>>(a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? PV_OK : (int)e;
+}
+
+extern "C" int pv_decoder_conv4s_f16(const void *fm, const void *skip, const void *w, const void *bias, void *out,
+                                     int32_t n, int32_t hin, int32_t win, float slope, pv_stream_t stream) {
+    if (!fm || !skip || !w || !bias || !out || n < 0 || hin < 2 || win < 2) return PV_EINVAL;
+    if (!(slope >= 0.f && slope < 1.f)) return PV_EINVAL;
+    if (((uintptr_t)fm | (uintptr_t)skip | (uintptr_t)w | (uintptr_t)out) % 16 || (uintptr_t)bias % 8)
+        return PV_EALIGN;
+    if (n == 0) return PV_OK;
+    DecConvArgs a;
+    a.fm = (const _Float16 *)fm; a.skip = (const _Float16 *)skip; a.w = (const _Float16 *)w;
+    a.bias = (const _Float16 *)bias; a.out = (_Float16 *)out;
+    a.N = n; a.Hin = hin; a.Win = win; a.H = 2 * hin; a.W = 2 * win;
+    if ((int64_t)a.H * a.W * kECo * 2 >= (1ll << 31) || (int64_t)hin * win * kEC1 * 2 >= (1ll << 31)) return PV_EINVAL;
+    a.tiles_r = (a.H + kTR - 1) / kTR;
+    a.tiles_c = (a.W + kTC - 1) / kTC;
+    const int64_t nt = (int64_t)n * a.tiles_r * a.tiles_c;
+    if (nt >= (1ll << 31)) return PV_EINVAL;
+    a.ntiles = (int)nt;
+    a.rh = (float)(hin - 1) / (float)(a.H - 1);
+    a.rw = (float)(win - 1) / (float)(a.W - 1);
+    a.slope = slope;
+    const int64_t grid = std::min<int64_t>(nt, cu_count_dec());   // persistent: one block per CU
+    k_dec_conv4s<<<(unsigned)grid, 512, 0, (hipStream_t)stream>>>(a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? PV_OK : (int)e;
 }

@@ -328,6 +328,35 @@ def decoder_conv2s(fm: torch.Tensor, skip: torch.Tensor, weights, slope: float =
     return out
 
 
+def decoder_conv4s_weights(c: nn.Conv2d):
+    """conv4s's 3x3 weights (BN folded, 192 -> 64) in ``pv_decoder_conv4s_f16``'s
+    layout [3][9][8][2][32][8] fp16 and its bias (fp16)."""
+    if c.kernel_size != (3, 3) or c.in_channels != 192 or c.out_channels != 64 or c.padding != (1, 1):
+        raise RuntimeError("decoder_conv4s: conv4s must be a 3x3, 192 -> 64, padding-1 convolution")
+    w = c.weight.detach().float()                                            # [64, 192, 3, 3]
+    w = w.reshape(2, 32, 3, 8, 8, 3, 3).permute(2, 5, 6, 3, 0, 1, 4)       # [p, ky, kx, q, m, c, j]
+    return w.reshape(3, 9, 8, 2, 32, 8).contiguous().half(), c.bias.detach().half().contiguous()
+
+
+def decoder_conv4s(fm: torch.Tensor, skip: torch.Tensor, weights, slope: float = 0.1) -> torch.Tensor:
+    """up8sto4s + torch.cat([fm, x4s], 1) + conv4s (MR:35-43) in one fp16
+    matrix-core pass (``pv_decoder_conv4s_f16``): fm [n, 128, h, w] and skip
+    [n, 64, 2h, 2w] channels_last float16 CUDA.  Returns [n, 64, 2h, 2w]."""
+    n, c, h, w = fm.shape
+    cl = torch.channels_last
+    if fm.dtype != torch.float16 or skip.dtype != torch.float16 or not fm.is_cuda:
+        raise RuntimeError("decoder_conv4s: float16 CUDA maps required")
+    if c != 128 or tuple(skip.shape) != (n, 64, 2 * h, 2 * w):
+        raise RuntimeError("decoder_conv4s: fm [n, 128, h, w] and skip [n, 64, 2h, 2w] required")
+    if not fm.is_contiguous(memory_format=cl) or not skip.is_contiguous(memory_format=cl):
+        raise RuntimeError("decoder_conv4s: channels_last maps required")
+    wt, b = weights
+    out = torch.empty((n, 64, 2 * h, 2 * w), dtype=fm.dtype, device=fm.device, memory_format=cl)
+    _dev_call("pv_decoder_conv4s_f16", None, fm, fm.data_ptr(), skip.data_ptr(), wt.data_ptr(), b.data_ptr(),
+              out.data_ptr(), n, h, w, float(slope))
+    return out
+
+
 def decoder_tail_weights(c0: nn.Conv2d, c1: nn.Conv2d, cin: int = 35):
     """convraw's weights (MR:53-58, BN folded into ``c0``) laid out for
     ``pv_decoder_tail_f16`` (include/pvvote.h): w1 [32][368] fp16 with
@@ -479,8 +508,17 @@ class PVNetInference(nn.Module):
         else:
             cat8 = conv_epilogue(_conv(y, r.fc[0]), r.fc[0].bias, "relu", skip=x8s)
         fm = conv_epilogue(_conv(cat8, self.conv8s[0]), self.conv8s[0].bias, "leaky")
-        fm = upsample2x_cat(fm, x4s, fm.shape[1] + x4s.shape[1])
-        fm = conv_epilogue(_conv(fm, self.conv4s[0]), self.conv4s[0].bias, "leaky")
+        c4 = self.conv4s[0]
+        if (fm.dtype == torch.float16 and self.fused_conv and fm.shape[1] == 128 and x4s.shape[1] == 64
+                and c4.in_channels == 192 and c4.out_channels == 64 and c4.kernel_size == (3, 3)):
+            key = (c4.weight.data_ptr(), c4.weight._version, c4.bias.data_ptr())
+            if getattr(self, "_c4s_key", None) != key:
+                self._c4s_w = decoder_conv4s_weights(c4)
+                self._c4s_key = key
+            fm = decoder_conv4s(fm, x4s, self._c4s_w, self.conv4s[2].negative_slope)
+        else:
+            fm = upsample2x_cat(fm, x4s, fm.shape[1] + x4s.shape[1])
+            fm = conv_epilogue(_conv(fm, c4), c4.bias, "leaky")
         c2 = self.conv2s[0]
         if (fm.dtype == torch.float16 and self.fused_conv and fm.shape[1] == 64 and x2s.shape[1] == 64
                 and c2.in_channels == 128 and c2.out_channels == 32 and c2.kernel_size == (3, 3)):

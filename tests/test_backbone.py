@@ -560,3 +560,58 @@ def test_decoder_conv2s_matches_torch(hw, device):
     print(f"decoder conv2s {2 * h}x{2 * w}: max dev {float(d.max()):.3e}, mean {float(d.mean()):.2e} (scale {sc:.2f})")
     assert float(d.max()) <= 2 ** -7 * sc
     assert float(d.mean()) <= 2 ** -12 * sc
+
+
+def test_decoder_conv_weight_layouts():
+    """The host-side weight images of pv_decoder_conv2s_f16 / _conv4s_f16
+    follow include/pvvote.h's index formulas (CPU)."""
+    from pvnet_amd.network import decoder_conv2s_weights, decoder_conv4s_weights
+    g = torch.Generator().manual_seed(5)
+    c4 = torch.nn.Conv2d(192, 64, 3, 1, 1)
+    c2 = torch.nn.Conv2d(128, 32, 3, 1, 1)
+    with torch.no_grad():
+        c4.weight.copy_(torch.randn(64, 192, 3, 3, generator=g))
+        c2.weight.copy_(torch.randn(32, 128, 3, 3, generator=g))
+    w4, _ = decoder_conv4s_weights(c4)
+    w2, _ = decoder_conv2s_weights(c2)
+    W4, W2 = c4.weight.detach().half(), c2.weight.detach().half()
+    for p in range(3):
+        for tap in range(9):
+            for q in range(8):
+                blk = W4[:, 64 * p + 8 * q: 64 * p + 8 * q + 8, tap // 3, tap % 3]          # [64, 8]
+                assert torch.equal(w4[p, tap, q].reshape(64, 8), blk)
+    for p in range(2):
+        for tap in range(9):
+            for q in range(8):
+                assert torch.equal(w2[p, tap, q], W2[:, 64 * p + 8 * q: 64 * p + 8 * q + 8, tap // 3, tap % 3])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hw", [(13, 21), (60, 80)])
+def test_decoder_conv4s_matches_torch(hw, device):
+    """pv_decoder_conv4s_f16 (up8sto4s + cat([fm, x4s]) + conv4s, MR:35-43)
+    against ATen's unfused fp16 ops; tolerance as the conv2s test."""
+    from pvnet_amd.network import decoder_conv4s, decoder_conv4s_weights
+    F = torch.nn.functional
+    g = torch.Generator().manual_seed(hw[0] * 17 + hw[1])
+    cl = torch.channels_last
+    n, (h, w) = 2, hw
+    fm = (torch.randn(n, 128, h, w, generator=g) * 2).to(device, torch.float16).contiguous(memory_format=cl)
+    skip = torch.randn(n, 64, 2 * h, 2 * w, generator=g).to(device, torch.float16).contiguous(memory_format=cl)
+    c = torch.nn.Conv2d(192, 64, 3, 1, 1).to(device)
+    with torch.no_grad():
+        c.weight.copy_(torch.randn(64, 192, 3, 3, generator=g) * 0.04)
+        c.bias.copy_(torch.randn(64, generator=g) * 0.5)
+    c = c.half()
+    with torch.no_grad():
+        up = F.interpolate(fm, scale_factor=2, mode="bilinear", align_corners=True)
+        y = F.conv2d(torch.cat([up, skip], 1), c.weight, None, 1, 1) + c.bias.view(1, -1, 1, 1)
+        ref = F.leaky_relu(y, 0.1)
+        got = decoder_conv4s(fm, skip, decoder_conv4s_weights(c), 0.1)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape and got.is_contiguous(memory_format=cl)
+    sc = float(ref.abs().max())
+    d = (got.float() - ref.float()).abs()
+    print(f"decoder conv4s {2 * h}x{2 * w}: max dev {float(d.max()):.3e}, mean {float(d.mean()):.2e} (scale {sc:.2f})")
+    assert float(d.max()) <= 2 ** -7 * sc
+    assert float(d.mean()) <= 2 ** -12 * sc
