@@ -238,11 +238,22 @@ int pv_conv_epilogue_f32(const void *x, const void *bias, const void *res, const
  * maxpool 3x3 / stride 2 / pad 1) for channels-last maps, BN folded into bias: x2s = relu(x + bias)
  * [n][h][w][c] and pool = maxpool(x2s) [n][(h-1)/2+1][(w-1)/2+1][c] in one pass.  x: the convolution's
  * output without bias; bias [c]; fp16: c a multiple of 8, f32: of 4; pointers 16-byte aligned, the three
- * maps distinct.  Both outputs equal ATen's bias add + ReLU + max_pool2d bit for bit. */
+ * maps distinct.  Both outputs equal ATen's bias add + ReLU + max_pool2d bit for bit.  bias and x2s
+ * both NULL: pool-only (x is x2s already, e.g. from pv_stem_conv_f16). */
 int pv_relu_maxpool_f16(const void *x, const void *bias, void *x2s, void *pool, int32_t n, int32_t h, int32_t w,
                         int32_t c, pv_stream_t stream);
 int pv_relu_maxpool_f32(const void *x, const void *bias, void *x2s, void *pool, int32_t n, int32_t h, int32_t w,
                         int32_t c, pv_stream_t stream);
+
+/* replaces the stem's convolution (lib/networks/resnet.py:139-142, 201-203: conv1 7x7 / stride 2 /
+ * pad 3, 3 -> 64 channels, bn1 folded into w / bias, relu) for a channels-last fp16 batch:
+ * img [n][h][wd][3] (h, wd even, 4-byte aligned), out = x2s [n][h/2][wd/2][64] (16-byte aligned).
+ * w: the folded weights in the kernel's space-to-depth layout [2][16 taps (ty, tx)][2][32][8] fp16
+ * (pvnet_amd.network.stem_weights: tap (ty, tx) channel dy*6 + dx*3 + c = W[c][2ty+dy-1][2tx+dx-1]),
+ * bias [64] fp16.  Roundings: the f32 sum rounded to fp16, + bias, ReLU (as ATen's conv then bias
+ * add and relu; the sum's order differs from MIOpen's). */
+int pv_stem_conv_f16(const void *img, const void *w, const void *bias, void *out, int32_t n, int32_t h, int32_t wd,
+                     pv_stream_t stream);
 
 /* replaces convraw's tail (model_repository.py:53-58 after the 3x3 convolution): BN bias + LeakyReLU(slope)
  * + the 1x1 convolution to seg_dim + ver_dim channels with its bias, one pass.  x: [P][cin] channels-last

@@ -1109,3 +1109,177 @@ extern "C" int pv_decoder_conv4s_f16(const void *fm, const void *skip, const voi
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? PV_OK : (int)e;
 }
+
+
+// ==========================================================================
+// The stem's convolution (RN:139-142: conv1 7x7 / 2 / pad 3, 3 -> 64 channels,
+// BN folded, ReLU -> x2s) on the matrix cores.  A stride-2 7x7 convolution is
+// a stride-1 4x4 one over the image folded 2 x 2 into its channels
+// (space-to-depth): s2d pixel (Y, X) holds image pixels (2Y + dy, 2X + dx) as
+// channels dy*6 + dx*3 + c (12, padded to 16), and
+//     x2s(y, x) = relu(b + sum_{ty,tx} W2[ty][tx] . s2d(y - 2 + ty, x - 2 + tx)),
+//     W2[ty][tx][dy*6 + dx*3 + c] = W[c][2ty + dy - 1][2tx + dx - 1]
+// (zero outside 0..6).  One tap = 16 channels = one v_mfma_f32_32x32x16_f16
+// per 32 output channels: 32 per wave and tile.  In the image's channels-last
+// fp16 layout the 6 channels of an s2d pixel's row dy are 12 contiguous bytes,
+// so a pixel is two 12-byte loads.
+// Persistent blocks of 8 waves (wave = output row, 32 pixels x 64 channels);
+// an 8 x 32 output tile reads an 11 x 35 s2d halo (12.3 KB in LDS, double
+// buffered; its two 16-byte granules per pixel swapped on odd 8-pixel groups:
+// conflict-free); halo pixels are loaded into registers two tiles ahead; the
+// weights (32 KB) stay in registers for the launch.  Epilogue: fp16 round,
+// + b, ReLU (as k_relu_pool), through LDS to 16-byte stores (a wave's output
+// row is 4 KB contiguous).  The maxpool after it is pv_relu_maxpool_f16's
+// pool-only form.
+// ==========================================================================
+constexpr int kSR = 8, kSC = 32;                      // output tile
+constexpr int kSHR = kSR + 3, kSHC = kSC + 3;         // s2d halo: 11 x 35
+constexpr int kSHalo = kSHR * kSHC;                   // 385 pixels
+constexpr int kSCo = 64;
+typedef unsigned int u3 __attribute__((ext_vector_type(3)));
+
+struct StemArgs {
+    const _Float16 *img;    // [N][H][W][3]
+    const _Float16 *w;      // [2 cout halves][16 taps][2 k halves][32 couts][8]: the lanes' A fragments
+    const _Float16 *bias;   // [64]
+    _Float16 *out;          // [N][H/2][W/2][64]
+    int N, H, W, Ho, Wo, tiles_r, tiles_c, ntiles;
+};
+
+__device__ __forceinline__ int stem_slot(int hp, int g) { return hp * 2 + (g ^ ((hp >> 3) & 1)); }
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_stem(StemArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t halo2[2][kSHalo * 32];
+    __shared__ __attribute__((aligned(16))) uint8_t obuf[8][kSC * kSCo * 2];   // each wave's 32 x 64 outputs
+    const int t = (int)threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int n = lane & 31, h = lane >> 5;
+    h8 wf[2][16];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int tap = 0; tap < 16; ++tap) wf[m][tap] = *(const h8 *)(a.w + (((m * 16 + tap) * 2 + h) * 32 + n) * 8);
+    h4 bq[2][4];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) bq[m][g] = *(const h4 *)(a.bias + 32 * m + 8 * g + 4 * h);
+    __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0): no weight waits inside the tile loop
+    auto coords = [&](int tile, int &b, int &y0, int &x0) {
+        const int tc = tile % a.tiles_c, rest = tile / a.tiles_c;
+        b = rest / a.tiles_r;
+        y0 = (rest % a.tiles_r) * kSR;
+        x0 = tc * kSC;
+    };
+    // this thread's halo pixel (t < 385): rows 2Y and 2Y + 1, 12 bytes each;
+    // two tiles ahead (a tile's MFMAs are shorter than a load's latency), in
+    // two register sets A and B that alternate
+    const int hy = t / kSHC, hx = t - hy * kSHC;
+    u3 a0 = {}, a1 = {}, b0 = {}, b1 = {};
+    // (issued for every tile, past the last as well -- with no access -- so the
+    // count of loads in flight is the same on every path)
+    auto fetch = [&](int tile, u3 &r0, u3 &r1) {
+        int b, y0, x0;
+        coords(min(tile, a.ntiles - 1), b, y0, x0);
+        const __amdgpu_buffer_rsrc_t ir = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(a.img + (int64_t)b * a.H * a.W * 3), 0, a.H * a.W * 6, 0x00020000);
+        const int Y = y0 - 2 + hy, X = x0 - 2 + hx;
+        const bool ok = tile < a.ntiles && t < kSHalo && Y >= 0 && 2 * Y < a.H && X >= 0 && 2 * X < a.W;
+        const uint32_t off = ok ? (uint32_t)((2 * Y * a.W + 2 * X) * 6) : 0x80000000u;
+        const uint32_t off1 = ok ? off + (uint32_t)(a.W * 6) : 0x80000000u;
+        r0 = __builtin_bit_cast(u3, __builtin_amdgcn_raw_buffer_load_b96(ir, off, 0, 0));
+        r1 = __builtin_bit_cast(u3, __builtin_amdgcn_raw_buffer_load_b96(ir, off1, 0, 0));
+    };
+    auto put = [&](uint8_t *halo, const u3 &r0, const u3 &r1) {
+        if (t < kSHalo) {
+            *(u4 *)(halo + stem_slot(t, 0) * 16) = u4{r0.x, r0.y, r0.z, r1.x};
+            *(u4 *)(halo + stem_slot(t, 1) * 16) = u4{r1.y, r1.z, 0u, 0u};
+        }
+    };
+    const int G = (int)gridDim.x;
+    uint8_t *ob = obuf[wid];
+    // Tile i: tile i + 2's loads, tile i's MFMAs, tile i + 1's halo into the
+    // other buffer (its loads issued a tile earlier), tile i's outputs through
+    // LDS to 16-byte stores (a wave's output row is 4 KB contiguous), one
+    // barrier.
+    auto step = [&](int tile, const uint8_t *halo, uint8_t *next, u3 &f0, u3 &f1, const u3 &p0, const u3 &p1) {
+        int b, y0, x0;
+        coords(tile, b, y0, x0);
+        __syncthreads();                      // this halo written; the reads of the other done
+        fetch(tile + 2 * G, f0, f1);
+        f16x acc0 = {}, acc1 = {};
+#pragma unroll
+        for (int tap = 0; tap < 16; ++tap) {
+            const int ty = tap >> 2, tx = tap & 3;
+            const h8 bf = *(const h8 *)(halo + stem_slot((wid + ty) * kSHC + n + tx, h) * 16);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[0][tap], bf, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[1][tap], bf, acc1, 0, 0, 0);
+        }
+        if (tile + G < a.ntiles) put(next, p0, p1);
+        // rows (i & 3) + 8 (i >> 2) + 4 h of acc = channels, column n = pixel:
+        // 8-byte pieces into the wave's LDS rows (16-byte chunk c of pixel n at
+        // c ^ (n & 7): conflict-free both ways), read back as 16 bytes per lane
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                h4 y;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const _Float16 v = (_Float16)((float)(_Float16)(m ? acc1 : acc0)[4 * g + j] + (float)bq[m][g][j]);
+                    y[j] = (float)v > 0.f ? v : (_Float16)0.f;
+                }
+                *(h4 *)(ob + n * 128 + (((4 * m + g) ^ (n & 7)) * 16) + 8 * h) = y;
+            }
+        __builtin_amdgcn_wave_barrier();
+        const int oy = y0 + wid;
+        const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(a.out + (int64_t)b * a.Ho * a.Wo * kSCo), 0, a.Ho * a.Wo * kSCo * 2, 0x00020000);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int p = 8 * r + (lane >> 3), q = lane & 7, ox = x0 + p;
+            const u4 v = *(const u4 *)(ob + p * 128 + ((q ^ (p & 7)) * 16));
+            const uint32_t po = oy < a.Ho && ox < a.Wo ? (uint32_t)(((oy * a.Wo + ox) * kSCo) * 2 + q * 16) : 0x80000000u;
+            __builtin_amdgcn_raw_buffer_store_b128(v, orr, po, 0, 0);
+        }
+    };
+    int tile = (int)blockIdx.x;
+    if (tile >= a.ntiles) return;
+    fetch(tile, a0, a1);
+    fetch(tile + G, b0, b1);
+    {   // four dropped stores (out-of-range offset), as a step ends with: the
+        // loop is entered with the same memory operations in flight as it
+        // repeats with, so the compiler's wait before the first put() is for
+        // that tile's loads only (vmcnt(6)), not for the last stores as well
+        const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc((void *)a.out, 0, 0, 0x00020000);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) __builtin_amdgcn_raw_buffer_store_b128(u4{0u, 0u, 0u, 0u}, orr, 0x80000000u + 16u * r, 0, 0);
+    }
+    put(halo2[0], a0, a1);
+    while (true) {
+        step(tile, halo2[0], halo2[1], a0, a1, b0, b1);
+        if ((tile += G) >= a.ntiles) break;
+        step(tile, halo2[1], halo2[0], b0, b1, a0, a1);
+        if ((tile += G) >= a.ntiles) break;
+    }
+}
+
+extern "C" int pv_stem_conv_f16(const void *img, const void *w, const void *bias, void *out, int32_t n, int32_t h,
+                                int32_t wd, pv_stream_t stream) {
+    if (!img || !w || !bias || !out || n < 0 || h < 2 || wd < 2 || h % 2 || wd % 2) return PV_EINVAL;
+    if (((uintptr_t)w | (uintptr_t)out) % 16 || (uintptr_t)bias % 8 || (uintptr_t)img % 4) return PV_EALIGN;
+    if (n == 0) return PV_OK;
+    if ((int64_t)h * wd * 6 >= (1ll << 31) || (int64_t)h * wd * kSCo / 2 >= (1ll << 31)) return PV_EINVAL;
+    StemArgs a;
+    a.img = (const _Float16 *)img; a.w = (const _Float16 *)w; a.bias = (const _Float16 *)bias;
+    a.out = (_Float16 *)out;
+    a.N = n; a.H = h; a.W = wd; a.Ho = h / 2; a.Wo = wd / 2;
+    a.tiles_r = (a.Ho + kSR - 1) / kSR;
+    a.tiles_c = (a.Wo + kSC - 1) / kSC;
+    const int64_t nt = (int64_t)n * a.tiles_r * a.tiles_c;
+    if (nt >= (1ll << 31)) return PV_EINVAL;
+    a.ntiles = (int)nt;
+    const int64_t grid = std::min<int64_t>(nt, cu_count_dec());   // persistent: one block per CU
+    k_stem<<<(unsigned)grid, 512, 0, (hipStream_t)stream>>>(a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? PV_OK : (int)e;
+}

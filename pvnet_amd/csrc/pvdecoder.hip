@@ -170,7 +170,8 @@ int epilogue(const void *x, const void *bias, const void *res, const void *rbias
 // pixel: it reads its 3x3 window of the conv output, writes the 2x2 of x2s it
 // owns (rows 2py, 2py + 1, columns 2px, 2px + 1 -- the owned blocks tile x2s)
 // and the window's max.  Roundings as k_epilogue; the max is exact, so both
-// maps equal ATen's bias add + ReLU + max_pool2d bit for bit.
+// maps equal ATen's bias add + ReLU + max_pool2d bit for bit.  Pool-only form
+// (bias and x2s NULL: x is x2s already, from pv_stem_conv_f16): the max alone.
 // --------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void k_relu_pool(const T *__restrict__ x, const T *__restrict__ bias,
@@ -186,7 +187,8 @@ __global__ __launch_bounds__(256) void k_relu_pool(const T *__restrict__ x, cons
         const int px = (int)(p % Wo);
         const int64_t q = p / Wo;
         const int py = (int)(q % Ho), b = (int)(q / Ho);
-        const vT bv = *(const vT *)(bias + V * k);
+        vT bv = {};
+        if (bias) bv = *(const vT *)(bias + V * k);
         vT m;
 #pragma unroll
         for (int e = 0; e < V; ++e) m[e] = (T)(-INFINITY);
@@ -202,11 +204,13 @@ __global__ __launch_bounds__(256) void k_relu_pool(const T *__restrict__ x, cons
                 vT v = *(const vT *)(x + off);
 #pragma unroll
                 for (int e = 0; e < V; ++e) {
-                    const T y = (T)((float)v[e] + (float)bv[e]);
-                    v[e] = (float)y > 0.f ? y : (T)0.f;
+                    if (bias) {
+                        const T y = (T)((float)v[e] + (float)bv[e]);
+                        v[e] = (float)y > 0.f ? y : (T)0.f;
+                    }
                     m[e] = (float)v[e] > (float)m[e] ? v[e] : m[e];
                 }
-                if (dy >= 0 && dx >= 0) *(vT *)(x2s + off) = v;
+                if (bias && dy >= 0 && dx >= 0) *(vT *)(x2s + off) = v;
             }
         }
         *(vT *)(pool + p * C + V * k) = m;
@@ -217,9 +221,10 @@ template <typename T>
 int relu_pool(const void *x, const void *bias, void *x2s, void *pool, int32_t n, int32_t h, int32_t w, int32_t c,
               pv_stream_t stream) {
     constexpr int V = 16 / sizeof(T);
-    if (!x || !bias || !x2s || !pool || n < 0 || h <= 0 || w <= 0 || c <= 0 || c % V) return PV_EINVAL;
+    if (!x || !pool || n < 0 || h <= 0 || w <= 0 || c <= 0 || c % V) return PV_EINVAL;
+    if (!bias != !x2s) return PV_EINVAL;   // both NULL: pool-only
     if (((uintptr_t)x | (uintptr_t)bias | (uintptr_t)x2s | (uintptr_t)pool) % 16) return PV_EALIGN;
-    if (x2s == x || pool == x || pool == x2s) return PV_EINVAL;
+    if (x2s == x || pool == x || (x2s && pool == x2s)) return PV_EINVAL;
     if (n == 0) return PV_OK;
     const int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;     // kernel 3, stride 2, pad 1
     const int64_t total = (int64_t)n * ho * wo * (c / V);

@@ -261,6 +261,61 @@ def relu_maxpool(y: torch.Tensor, bias: torch.Tensor):
     return x2s, pool
 
 
+def maxpool(x2s: torch.Tensor):
+    """maxpool 3x3 / 2 / 1 (RN:204) of a channels-last map in one HIP pass
+    (``pv_relu_maxpool_f16 / _f32``'s pool-only form): bit-equal to ATen's."""
+    n, c, h, w = x2s.shape
+    cl = torch.channels_last
+    if not x2s.is_contiguous(memory_format=cl):
+        raise RuntimeError("maxpool: channels_last input required")
+    pool = torch.empty((n, c, (h - 1) // 2 + 1, (w - 1) // 2 + 1), dtype=x2s.dtype, device=x2s.device,
+                       memory_format=cl)
+    _dev_call("pv_relu_maxpool_f16", "pv_relu_maxpool_f32", x2s, x2s.data_ptr(), None, None, pool.data_ptr(),
+              n, h, w, c)
+    return pool
+
+
+def stem_eligible(c: nn.Conv2d) -> bool:
+    """conv1 as ``pv_stem_conv_f16`` takes it: 7x7, stride 2, padding 3, 3 -> 64."""
+    return (c.kernel_size == (7, 7) and c.stride == (2, 2) and c.padding == (3, 3) and c.dilation == (1, 1)
+            and c.groups == 1 and c.in_channels == 3 and c.out_channels == 64)
+
+
+def stem_weights(c: nn.Conv2d):
+    """conv1's weights (BN folded) in ``pv_stem_conv_f16``'s space-to-depth
+    layout and its bias, fp16: tap (ty, tx) of the 4x4 convolution over 2x2-
+    folded pixels, channel dy*6 + dx*3 + ci = W[ci][2ty+dy-1][2tx+dx-1] (zero
+    outside the 7x7), as the lanes' A fragments [2][16][2][32][8]."""
+    if not stem_eligible(c):
+        raise RuntimeError("stem_weights: conv1 must be a 7x7 / 2 / pad 3, 3 -> 64 convolution")
+    w = c.weight.detach().float()                                   # [64, 3, 7, 7]
+    w8 = torch.zeros(64, 3, 8, 8, dtype=w.dtype, device=w.device)
+    w8[:, :, 1:, 1:] = w                                            # index 2t + d = k + 1
+    w2 = w8.reshape(64, 3, 4, 2, 4, 2).permute(0, 2, 4, 3, 5, 1)    # [co, ty, tx, dy, dx, ci]
+    w2 = torch.cat([w2.reshape(64, 16, 12), w2.new_zeros(64, 16, 4)], 2)   # [co, tap, 16]
+    w2 = w2.reshape(2, 32, 16, 2, 8).permute(0, 2, 3, 1, 4)        # [m, tap, h, n, 8]
+    b = c.bias.detach().half().contiguous() if c.bias is not None else torch.zeros(64, dtype=torch.half,
+                                                                                    device=w.device)
+    return w2.contiguous().half(), b
+
+
+def stem_conv(img: torch.Tensor, weights) -> torch.Tensor:
+    """relu(conv1(img) + b) (RN:139-142, 201-203; BN folded) as one fp16
+    matrix-core pass (``pv_stem_conv_f16``): img [n, 3, h, w] channels_last
+    float16 CUDA, h and w even; ``weights`` from :func:`stem_weights`.
+    Returns x2s [n, 64, h/2, w/2] channels_last."""
+    n, c, h, w = img.shape
+    if img.dtype != torch.float16 or not img.is_cuda or c != 3:
+        raise RuntimeError("stem_conv: a [n, 3, h, w] float16 CUDA image required")
+    if h % 2 or w % 2 or not img.is_contiguous(memory_format=torch.channels_last):
+        raise RuntimeError("stem_conv: channels_last, even h and w required")
+    wt, b = weights
+    out = torch.empty((n, 64, h // 2, w // 2), dtype=img.dtype, device=img.device,
+                      memory_format=torch.channels_last)
+    _dev_call("pv_stem_conv_f16", None, img, img.data_ptr(), wt.data_ptr(), b.data_ptr(), out.data_ptr(), n, h, w)
+    return out
+
+
 def conv3x3_eligible(c: nn.Conv2d) -> bool:
     """The convolutions ``pv_conv3x3_f16`` takes: 3x3, stride 1, padding =
     dilation, no groups, Cin a multiple of 64, Cout of 256 (layer3, layer4, fc)."""
@@ -485,7 +540,16 @@ class PVNetInference(nn.Module):
     def forward(self, x):
         r = self.resnet18_8s
         mp = r.maxpool
-        if (mp.kernel_size, mp.stride, mp.padding, mp.dilation, mp.ceil_mode) == (3, 2, 1, 1, False):
+        pool3 = (mp.kernel_size, mp.stride, mp.padding, mp.dilation, mp.ceil_mode) == (3, 2, 1, 1, False)
+        if (self.fused_conv and x.dtype == torch.float16 and stem_eligible(r.conv1) and x.shape[2] % 2 == 0
+                and x.shape[3] % 2 == 0):
+            key = (r.conv1.weight.data_ptr(), r.conv1.weight._version, r.conv1.bias.data_ptr())
+            if getattr(self, "_stem_key", None) != key:     # the kernel's weight layout, made once
+                self._stem_w = stem_weights(r.conv1)
+                self._stem_key = key
+            x2s = stem_conv(x, self._stem_w)
+            y = maxpool(x2s) if pool3 else mp(x2s)
+        elif pool3:
             x2s, y = relu_maxpool(_conv(x, r.conv1), r.conv1.bias)
         else:
             x2s = conv_epilogue(_conv(x, r.conv1), r.conv1.bias, "relu")

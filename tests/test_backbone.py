@@ -615,3 +615,63 @@ def test_decoder_conv4s_matches_torch(hw, device):
     print(f"decoder conv4s {2 * h}x{2 * w}: max dev {float(d.max()):.3e}, mean {float(d.mean()):.2e} (scale {sc:.2f})")
     assert float(d.max()) <= 2 ** -7 * sc
     assert float(d.mean()) <= 2 ** -12 * sc
+
+
+def test_stem_weight_layout():
+    """pv_stem_conv_f16's space-to-depth weights (network.stem_weights): the
+    4x4 convolution over 2x2-folded pixels they describe equals conv1's 7x7 /
+    stride 2 / pad 3 convolution (CPU, f64 emulation of the kernel's sum)."""
+    from pvnet_amd.network import stem_weights
+    F = torch.nn.functional
+    g = torch.Generator().manual_seed(11)
+    c = torch.nn.Conv2d(3, 64, 7, 2, 3)
+    with torch.no_grad():
+        c.weight.copy_(torch.randn(64, 3, 7, 7, generator=g))
+    wt, _ = stem_weights(c)
+    assert tuple(wt.shape) == (2, 16, 2, 32, 8)
+    W2 = wt.double().permute(0, 3, 1, 2, 4).reshape(64, 16, 16)       # [co, tap, s2d channel]
+    h, w = 10, 14
+    img = torch.randn(1, 3, h, w, generator=g, dtype=torch.float64)
+    # s2d pixel (Y, X), channel dy*6 + dx*3 + ci = img[ci][2Y + dy][2X + dx]; 2 pixels of zero border
+    s2d = img[0].reshape(3, h // 2, 2, w // 2, 2).permute(1, 3, 2, 4, 0).reshape(h // 2, w // 2, 12)
+    s2d = F.pad(torch.cat([s2d, s2d.new_zeros(h // 2, w // 2, 4)], 2), (0, 0, 2, 2, 2, 2))
+    got = torch.zeros(64, h // 2, w // 2, dtype=torch.float64)
+    for tap in range(16):
+        ty, tx = divmod(tap, 4)
+        got += torch.einsum("oc,yxc->oyx", W2[:, tap], s2d[ty:ty + h // 2, tx:tx + w // 2])
+    ref = F.conv2d(img, c.weight.detach().half().double(), None, 2, 3)[0]
+    assert torch.allclose(got, ref, atol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hw", [(480, 640), (38, 70)])
+def test_stem_conv_matches_torch(hw, device):
+    """pv_stem_conv_f16 (conv1 7x7/2/3 + folded BN + ReLU = x2s, RN:139-142,
+    201-203) against MIOpen's fp16 convolution + ATen's bias add and ReLU; then
+    the pool-only maxpool against max_pool2d (bit-equal on the same x2s).  Both
+    convolutions sum in f32 and round once to fp16 (in other orders): within a
+    couple of fp16 roundings of the convolution's scale; ragged tiles (19 x 35
+    outputs) included."""
+    from pvnet_amd.network import maxpool, stem_conv, stem_weights
+    F = torch.nn.functional
+    g = torch.Generator().manual_seed(hw[0] + hw[1])
+    cl = torch.channels_last
+    h, w = hw
+    img = torch.randn(2, 3, h, w, generator=g).to(device, torch.float16).contiguous(memory_format=cl)
+    c = torch.nn.Conv2d(3, 64, 7, 2, 3).to(device)
+    with torch.no_grad():
+        c.weight.copy_(torch.randn(64, 3, 7, 7, generator=g) * 0.1)
+        c.bias.copy_(torch.randn(64, generator=g) * 0.5)
+    c = c.half()
+    with torch.no_grad():
+        ref = torch.relu(F.conv2d(img, c.weight, None, 2, 3) + c.bias.view(1, -1, 1, 1))
+        got = stem_conv(img, stem_weights(c))
+        pool = maxpool(got)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape and got.is_contiguous(memory_format=cl)
+    sc = float(ref.abs().max())
+    d = (got.float() - ref.float()).abs()
+    print(f"stem conv {h}x{w}: max dev {float(d.max()):.3e}, mean {float(d.mean()):.2e} (scale {sc:.2f})")
+    assert float(d.max()) <= 2 ** -7 * sc
+    assert float(d.mean()) <= 2 ** -12 * sc
+    assert pool.is_contiguous(memory_format=cl) and torch.equal(pool, F.max_pool2d(got, 3, 2, 1))
