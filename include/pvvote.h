@@ -265,12 +265,12 @@ int pv_head_f32(const void *x, const float *b1, const float *w2, const float *b2
                 int32_t cin, int32_t cout, float slope, pv_stream_t stream);
 
 /* replaces, for the backbone's wide 3x3 convolutions (lib/networks/resnet.py:21-38 conv3x3 with
- * dilation, :167-198 layer3 / layer4; model_repository.py:22-26 fc), MIOpen's convolution + the
+ * dilation, :167-198 layer2 / layer3 / layer4; model_repository.py:22-35 fc, conv8s), MIOpen's convolution + the
  * epilogue pass after it: out = act(conv(x) + bias (+ (res + rbias))), fp16, channels-last, stride 1,
  * padding = dilation.  x [n][h][w][cin], w [cout][3][3][cin] (the conv weight permuted; BN folded),
  * bias / rbias [cout], res [n][h][w][cout], out [n][h][w][ldo] (channels [0, cout) written; ldo = 0:
  * cout -- ldo > cout writes into a wider map, e.g. the torch.cat after fc, MR:66).  res, rbias may be
- * NULL.  cin a multiple of 64, cout of 256, ldo of 4; x, w, res, out 16-byte, bias, rbias 8-byte
+ * NULL.  cin a multiple of 64, cout of 128, ldo of 4; x, w, res, out 16-byte, bias, rbias 8-byte
  * aligned; out distinct from x and res.  act PV_ACT_*.  The sums are f32 (matrix cores) rounded to fp16,
  * then pv_conv_epilogue's roundings. */
 int pv_conv3x3_f16(const void *x, const void *w, const void *bias, const void *res, const void *rbias, void *out,

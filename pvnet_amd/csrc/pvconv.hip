@@ -386,9 +386,9 @@ unsigned long long *g_tail_trace = nullptr;
 
 
 // ==========================================================================
-// The backbone's wide 3x3 convolutions (layer3 / layer4 / fc: Cin a multiple
-// of 64, Cout a multiple of 256, stride 1, padding = dilation; RN:21-38,
-// 167-198, MR:22-26) as an implicit GEMM on v_mfma_f32_16x16x32_f16, with
+// The backbone's wide 3x3 convolutions (layer2 / layer3 / layer4 / fc /
+// conv8s: Cin a multiple of 64, Cout of 128, stride 1, padding = dilation;
+// RN:21-38, 167-198, MR:22-35) as an implicit GEMM on v_mfma_f32_16x16x32_f16, with
 // the conv epilogue (folded BN bias, residual, ReLU; k_epilogue's roundings)
 // fused.  D[cout][pixel] = sum_k W[cout][k] X[k][pixel], k = tap * Cin + c.
 //
@@ -403,11 +403,13 @@ unsigned long long *g_tail_trace = nullptr;
 // the loads' source addresses; the LDS side is lane-linear), which keeps the
 // fragments' ds_read_b128 conflict-free.  The accumulator's 4 registers are
 // 4 consecutive output channels of one pixel: an 8-byte store per lane.
+// Cout a multiple of 128 but not 256 (layer2, conv8s): 128-cout tiles (wave =
+// 32 couts x 64 pixels, 2 x 4 accumulators; 96 KiB of LDS).
 // ==========================================================================
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-constexpr int kCT = 256;                   // couts per tile
+constexpr int kCT = 256;                   // couts per tile (128 for Cout a multiple of 128 only)
 constexpr int kPT = 256;                   // pixels per tile
 
 struct ConvArgs {
@@ -436,14 +438,16 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_ba
 #endif
 constexpr int kNW = PVC_NW;                   // waves per block: 16 (4 cout x 4 pixel groups; 8 = 2 x 4 measured 5-8 % slower)
 
+template <int CT>
 __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
     constexpr int KB = 64;                                 // K-step: one tap x 64 input channels
     constexpr int RB = KB * 2;                             // bytes per LDS row
-    constexpr int STAGE = (kCT + kPT) * RB;                // 64 KiB
+    constexpr int STAGE = (CT + kPT) * RB;                 // 64 KiB (CT 256), 48 KiB (CT 128)
     constexpr int GPR = RB / 16;                           // 16-byte granules per row
-    constexpr int NI = (kCT * RB) / (1024 * kNW);          // buffer-to-LDS loads per wave per operand per stage
+    constexpr int NI = (kPT * RB) / (1024 * kNW);          // pixel buffer-to-LDS loads per wave per stage
+    constexpr int NW = (CT * RB) / (1024 * kNW);           // weight loads per wave per stage
     constexpr int WC = kNW / 4;                            // cout groups of waves
-    constexpr int MI = kCT / WC / 16;                      // 16-cout accumulator tiles per wave
+    constexpr int MI = CT / WC / 16;                       // 16-cout accumulator tiles per wave
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STAGE];
     const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
     // XCD-aware tile order: blocks i, i + 8, ... share an XCD; give each XCD a
@@ -454,7 +458,7 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
         bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
     }
     const int ct = bid / a.ntp, pt = bid % a.ntp;
-    const int n0 = ct * kCT;
+    const int n0 = ct * CT;
     const int64_t p0 = (int64_t)pt * kPT;
     const __amdgpu_buffer_rsrc_t wr =
         __builtin_amdgcn_make_buffer_rsrc((void *)a.w, 0, (int)((int64_t)a.Cout * 9 * a.Cin * 2), 0x00020000);
@@ -463,15 +467,20 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
     const int K2 = 9 * a.Cin * 2;            // bytes per weight row
     const int cbk = a.Cin / KB;              // channel blocks per tap
     const int ksteps = 9 * cbk;
-    // this lane's NI weight and NI pixel granules per stage: granule g = (NI wid + i) 64 + lane
-    int woff[NI], py[NI], px[NI];
+    // this lane's NW weight and NI pixel granules per stage: granule g = (N wid + i) 64 + lane
+    int woff[NW], py[NI], px[NI];
     int64_t pbase[NI];
     bool pin[NI];
 #pragma unroll
-    for (int i = 0; i < NI; ++i) {
-        const int g = (NI * wid + i) * 64 + lane, row = g / GPR, pseg = g % GPR;
+    for (int i = 0; i < NW; ++i) {
+        const int g = (NW * wid + i) * 64 + lane, row = g / GPR, pseg = g % GPR;
         const int seg = conv_granule(row, pseg) - row * GPR;   // the swizzle is an involution per row
         woff[i] = (n0 + row) * K2 + seg * 16;
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int g = (NI * wid + i) * 64 + lane, row = g / GPR, pseg = g % GPR;
+        const int seg = conv_granule(row, pseg) - row * GPR;
         const int64_t p = p0 + row;
         pin[i] = p < a.M;
         const int64_t pc = pin[i] ? p : 0;
@@ -484,8 +493,8 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
         const int tap = s / cbk, cb = s - tap * cbk;
         uint8_t *st = lds + buf * STAGE;
 #pragma unroll
-        for (int i = 0; i < NI; ++i)
-            glds16(wr, st + (NI * wid + i) * 1024, woff[i], (tap * a.Cin + cb * KB) * 2);
+        for (int i = 0; i < NW; ++i)
+            glds16(wr, st + (NW * wid + i) * 1024, woff[i], (tap * a.Cin + cb * KB) * 2);
     };
     auto issue_x = [&](int s, int buf) {
         const int tap = s / cbk, cb = s - tap * cbk;
@@ -496,7 +505,7 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
         for (int i = 0; i < NI; ++i) {
             const bool ok = pin[i] && (unsigned)(py[i] + dy) < (unsigned)a.H && (unsigned)(px[i] + dx) < (unsigned)a.W;
             const uint32_t off = ok ? (uint32_t)(pbase[i] + dpix) : 0x80000000u;
-            glds16(xr, st + kCT * RB + (NI * wid + i) * 1024, off, 0);
+            glds16(xr, st + CT * RB + (NI * wid + i) * 1024, off, 0);
         }
     };
     auto issue = [&](int s, int buf) { issue_w(s, buf); issue_x(s, buf); };
@@ -519,7 +528,7 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni) {
                 const int r = wm * 64 + ni * 16 + (lane & 15);
-                bf[ni] = *(const h8v *)(st + kCT * RB + conv_granule(r, sg) * 16);
+                bf[ni] = *(const h8v *)(st + CT * RB + conv_granule(r, sg) * 16);
             }
 #ifdef PVC_NO_MFMA
 #pragma unroll
@@ -1033,7 +1042,7 @@ extern "C" int pv_conv3x3_f16(const void *x, const void *w, const void *bias, co
                               void *out, int32_t ldo, int32_t n, int32_t h, int32_t wd, int32_t cin, int32_t cout,
                               int32_t dil, int32_t act, float slope, pv_stream_t stream) {
     if (!x || !w || !bias || !out || n < 0 || h <= 0 || wd <= 0 || dil < 1 || act < 0 || act > 2) return PV_EINVAL;
-    if (cin <= 0 || cin % 64 || cout <= 0 || cout % kCT || (rbias && !res)) return PV_EINVAL;
+    if (cin <= 0 || cin % 64 || cout <= 0 || cout % 128 || (rbias && !res)) return PV_EINVAL;
     if (ldo == 0) ldo = cout;
     if (ldo < cout || ldo % 4) return PV_EINVAL;
     if (((uintptr_t)x | (uintptr_t)w | (uintptr_t)out | (uintptr_t)res) % 16 || ((uintptr_t)bias | (uintptr_t)rbias) % 8)
@@ -1051,9 +1060,11 @@ extern "C" int pv_conv3x3_f16(const void *x, const void *w, const void *bias, co
     a.cblocks = cin / 64;
     a.ksteps = 9 * a.cblocks;
     a.ntp = (int)((a.M + kPT - 1) / kPT);
-    a.nct = cout / kCT;
+    const bool wide = cout % kCT == 0;       // 256-cout tiles, else 128
+    a.nct = cout / (wide ? kCT : 128);
     a.ntiles = a.ntp * a.nct;
-    k_conv3x3<<<(unsigned)a.ntiles, 64 * kNW, 0, (hipStream_t)stream>>>(a);
+    if (wide) k_conv3x3<kCT><<<(unsigned)a.ntiles, 64 * kNW, 0, (hipStream_t)stream>>>(a);
+    else k_conv3x3<128><<<(unsigned)a.ntiles, 64 * kNW, 0, (hipStream_t)stream>>>(a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? PV_OK : (int)e;
 }

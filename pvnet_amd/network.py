@@ -318,9 +318,10 @@ def stem_conv(img: torch.Tensor, weights) -> torch.Tensor:
 
 def conv3x3_eligible(c: nn.Conv2d) -> bool:
     """The convolutions ``pv_conv3x3_f16`` takes: 3x3, stride 1, padding =
-    dilation, no groups, Cin a multiple of 64, Cout of 256 (layer3, layer4, fc)."""
+    dilation, no groups, Cin a multiple of 64, Cout of 128 (layer2's stride-1
+    convolutions, layer3, layer4, fc, conv8s)."""
     return (c.kernel_size == (3, 3) and c.stride == (1, 1) and c.groups == 1 and c.padding == c.dilation
-            and c.dilation[0] == c.dilation[1] and c.in_channels % 64 == 0 and c.out_channels % 256 == 0)
+            and c.dilation[0] == c.dilation[1] and c.in_channels % 64 == 0 and c.out_channels % 128 == 0)
 
 
 def conv3x3(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, dil: int, act: str = "relu",
@@ -571,7 +572,7 @@ class PVNetInference(nn.Module):
             cat8[:, c.out_channels:].copy_(x8s)
         else:
             cat8 = conv_epilogue(_conv(y, r.fc[0]), r.fc[0].bias, "relu", skip=x8s)
-        fm = conv_epilogue(_conv(cat8, self.conv8s[0]), self.conv8s[0].bias, "leaky")
+        fm = self._conv_act(self.conv8s[0], cat8, "leaky")
         c4 = self.conv4s[0]
         if (fm.dtype == torch.float16 and self.fused_conv and fm.shape[1] == 128 and x4s.shape[1] == 64
                 and c4.in_channels == 192 and c4.out_channels == 64 and c4.kernel_size == (3, 3)):

@@ -487,14 +487,16 @@ def test_relu_maxpool_matches_torch(dtype, hw, device):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["relu_128_256_d2", "res_256_256_d2", "resb_256_512_d4", "relu_512_512_d4",
-                                  "fc_512_256_d1_ragged", "leaky_64_256_d1"])
+                                  "fc_512_256_d1_ragged", "leaky_64_256_d1", "resb_128_128_d1",
+                                  "leaky_384_128_d1_ragged"])
 def test_conv3x3_matches_torch(case, device):
     """pv_conv3x3_f16 (the wide 3x3 convolutions of layer3 / layer4 / fc with
     their epilogue, RN:21-38 / MR:22-26) against MIOpen's fp16 convolution +
     ATen's bias / residual / activation on the same inputs.  Both sum in f32
     and round the convolution to fp16 (in other orders), so the outputs agree
     within a couple of fp16 roundings of the convolution's scale; padding,
-    dilation and a pixel count that is not a multiple of the tile included."""
+    dilation, a pixel count that is not a multiple of the tile and the
+    128-cout tiles (layer2, conv8s) included."""
     from pvnet_amd.network import conv3x3, conv3x3_weight
     F = torch.nn.functional
     kind, cin, cout, d = case.split("_")[0], *[int(v) for v in case.split("_")[1:3]], int(case.split("_")[3][1:])
