@@ -255,6 +255,15 @@ int pv_relu_maxpool_f32(const void *x, const void *bias, void *x2s, void *pool, 
 int pv_stem_conv_f16(const void *img, const void *w, const void *bias, void *out, int32_t n, int32_t h, int32_t wd,
                      pv_stream_t stream);
 
+/* replaces, for layer1's convolutions (lib/networks/resnet.py:21-70 BasicBlock conv1 / conv2 at
+ * 64 -> 64 channels, 3x3, stride 1, pad 1), MIOpen's convolution + the epilogue pass after it:
+ * out = act(conv(x) + bias (+ res)), fp16 channels-last, x / res / out [n][h][wd][64].  w: the folded
+ * weights as [9 taps (ky, kx)][8 octets q][64 couts][8] fp16 = W[cout][8q + j][ky][kx]
+ * (pvnet_amd.network.conv64_weights), bias [64].  act: PV_ACT_NONE or PV_ACT_RELU.  x, w, res, out
+ * 16-byte, bias 8-byte aligned; out distinct from x and res.  Roundings as pv_conv3x3_f16. */
+int pv_conv64_f16(const void *x, const void *w, const void *bias, const void *res, void *out, int32_t n, int32_t h,
+                  int32_t wd, int32_t act, pv_stream_t stream);
+
 /* replaces convraw's tail (model_repository.py:53-58 after the 3x3 convolution): BN bias + LeakyReLU(slope)
  * + the 1x1 convolution to seg_dim + ver_dim channels with its bias, one pass.  x: [P][cin] channels-last
  * (the 3x3 convolution's output without bias), b1 f32 [cin], w2 f32 [cout][cin], b2 f32 [cout] (device),

@@ -979,6 +979,117 @@ __global__ __launch_bounds__(512) void k_dec_conv4s(DecConvArgs a) {
     }
 }
 
+// ==========================================================================
+// layer1's convolutions (RN:21-70 BasicBlock, 64 -> 64 channels, 3x3, stride
+// 1, pad 1, at quarter resolution) with their epilogue (folded BN bias, the
+// residual, ReLU; k_epilogue's roundings), fp16 channels-last, one pass.  An
+// implicit GEMM would read each pixel nine times over for 64 output
+// channels; here the decoder kernels' halo structure: persistent blocks of 8
+// waves, one per CU; the weights (73.7 KB, [9 taps][8 octets][64][8]) resident
+// in LDS for the launch; an 8 x 32 output tile per step, its 10 x 34 x 64
+// halo copied into LDS (XOR-swizzled per pixel) from registers loaded during
+// the previous tile's convolution; per wave one output row: 36 k-steps x 2
+// v_mfma_f32_32x32x16_f16 (64 output channels).
+// ==========================================================================
+struct L1Args {
+    const _Float16 *x, *w, *bias, *res;   // res: [N][H][W][64] or null
+    _Float16 *out;
+    int N, H, W, tiles_r, tiles_c, ntiles, act;
+};
+
+__global__ __launch_bounds__(512) void k_conv64(L1Args a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[72 * 64 * 16 + kDHalo * 16];
+    uint8_t *wl = lds;                                  // 73,728 B
+    uint8_t *halo = lds + 72 * 64 * 16;                 // 43,520 B
+    const int t = (int)threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int n = lane & 31, h = lane >> 5;
+    for (int i = t; i < 72 * 64; i += 512) *(h8 *)(wl + i * 16) = *(const h8 *)(a.w + i * 8);
+    h4 bq[2][4];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) bq[m][g] = *(const h4 *)(a.bias + 32 * m + 8 * g + 4 * h);
+    auto coords = [&](int tile, int &b, int &y0, int &x0) {
+        const int tc = tile % a.tiles_c, rest = tile / a.tiles_c;
+        b = rest / a.tiles_r;
+        y0 = (rest % a.tiles_r) * kTR;
+        x0 = tc * kTC;
+    };
+    h8 pre[kDSkipIt];
+    auto fetch = [&](int tile) {
+        int b, y0, x0;
+        coords(tile, b, y0, x0);
+        const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(a.x + (int64_t)b * a.H * a.W * 64), 0, a.H * a.W * 128, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < kDSkipIt; ++i) {
+            const int c = min(t + 512 * i, kDHalo - 1), hp = c >> 3, q = c & 7;
+            const int hy = hp / kHC, hx = hp - hy * kHC;
+            const int oy = y0 - 1 + hy, ox = x0 - 1 + hx;
+            const bool ok = oy >= 0 && oy < a.H && ox >= 0 && ox < a.W;
+            const uint32_t off = ok ? (uint32_t)((oy * a.W + ox) * 128 + q * 16) : 0x80000000u;
+            pre[i] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+        }
+    };
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    int tile = (int)blockIdx.x;
+    if (tile < a.ntiles) fetch(tile);
+    for (; tile < a.ntiles; tile += (int)gridDim.x) {
+        int b, y0, x0;
+        coords(tile, b, y0, x0);
+        __syncthreads();                      // the previous tile's halo reads (and the weights) are done
+#pragma unroll
+        for (int i = 0; i < kDSkipIt; ++i) {
+            const int c = t + 512 * i;
+            if (c < kDHalo) *(h8 *)(halo + halo_granule(c >> 3, c & 7) * 16) = pre[i];
+        }
+        __syncthreads();
+        if (tile + (int)gridDim.x < a.ntiles) fetch(tile + (int)gridDim.x);
+        f16x acc[2] = {};
+#pragma unroll 4
+        for (int s = 0; s < 36; ++s) {
+            const int o = 2 * s + h;          // octet of this lane half: tap o / 8, channels 8 (o % 8)
+            const int tap = o >> 3, q = o & 7;
+            const int ky = tap / 3, kx = tap - 3 * ky;
+            const h8 bf = *(const h8 *)(halo + halo_granule((wid + ky) * kHC + n + kx, q) * 16);
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const h8 af = *(const h8 *)(wl + ((o * 2 + m) * 32 + n) * 16);
+                acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[m], 0, 0, 0);
+            }
+        }
+        // ---- epilogue: acc[m] rows (i & 3) + 8 (i >> 2) + 4 h = couts 32 m + .., column n = pixel ----
+        const int oy = y0 + wid, ox = x0 + n;
+        if (oy < a.H && ox < a.W) {
+            const int64_t po = (((int64_t)b * a.H + oy) * a.W + ox) * 64;
+            h4 r[2][4];
+            if (a.res) {
+#pragma unroll
+                for (int m = 0; m < 2; ++m)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) r[m][g] = *(const h4 *)(a.res + po + 32 * m + 8 * g + 4 * h);
+            }
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    h4 y;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) y[j] = (_Float16)((float)(_Float16)acc[m][4 * g + j] + (float)bq[m][g][j]);
+                    if (a.res) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) y[j] = (_Float16)((float)y[j] + (float)r[m][g][j]);
+                    }
+                    if (a.act == 1) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) y[j] = (float)y[j] > 0.f ? y[j] : (_Float16)0.f;
+                    }
+                    *(h4 *)(a.out + po + 32 * m + 8 * g + 4 * h) = y;
+                }
+        }
+    }
+}
+
 int cu_count_dec() {
     static int n = 0;
     if (!n) {
@@ -1291,6 +1402,28 @@ extern "C" int pv_stem_conv_f16(const void *img, const void *w, const void *bias
     a.ntiles = (int)nt;
     const int64_t grid = std::min<int64_t>(nt, cu_count_dec());   // persistent: one block per CU
     k_stem<<<(unsigned)grid, 512, 0, (hipStream_t)stream>>>(a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? PV_OK : (int)e;
+}
+
+extern "C" int pv_conv64_f16(const void *x, const void *w, const void *bias, const void *res, void *out, int32_t n,
+                             int32_t h, int32_t wd, int32_t act, pv_stream_t stream) {
+    if (!x || !w || !bias || !out || n < 0 || h <= 0 || wd <= 0 || act < 0 || act > 1) return PV_EINVAL;
+    if (((uintptr_t)x | (uintptr_t)w | (uintptr_t)out | (uintptr_t)res) % 16 || (uintptr_t)bias % 8) return PV_EALIGN;
+    if (out == x || (res && out == res)) return PV_EINVAL;
+    if (n == 0) return PV_OK;
+    if ((int64_t)h * wd * 128 >= (1ll << 31)) return PV_EINVAL;
+    L1Args a;
+    a.x = (const _Float16 *)x; a.w = (const _Float16 *)w; a.bias = (const _Float16 *)bias;
+    a.res = (const _Float16 *)res; a.out = (_Float16 *)out;
+    a.N = n; a.H = h; a.W = wd; a.act = act;
+    a.tiles_r = (h + kTR - 1) / kTR;
+    a.tiles_c = (wd + kTC - 1) / kTC;
+    const int64_t nt = (int64_t)n * a.tiles_r * a.tiles_c;
+    if (nt >= (1ll << 31)) return PV_EINVAL;
+    a.ntiles = (int)nt;
+    const int64_t grid = std::min<int64_t>(nt, cu_count_dec());   // persistent: one block per CU
+    k_conv64<<<(unsigned)grid, 512, 0, (hipStream_t)stream>>>(a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? PV_OK : (int)e;
 }

@@ -316,6 +316,41 @@ def stem_conv(img: torch.Tensor, weights) -> torch.Tensor:
     return out
 
 
+def conv64_eligible(c: nn.Conv2d) -> bool:
+    """The convolutions ``pv_conv64_f16`` takes: layer1's 3x3 / stride 1 / pad
+    1, 64 -> 64."""
+    return (c.kernel_size == (3, 3) and c.stride == (1, 1) and c.padding == (1, 1) and c.dilation == (1, 1)
+            and c.groups == 1 and c.in_channels == 64 and c.out_channels == 64)
+
+
+def conv64_weights(c: nn.Conv2d) -> torch.Tensor:
+    """A 64 -> 64 3x3 weight (BN folded) as ``pv_conv64_f16`` reads it: [9 taps
+    (ky, kx)][8 octets q][64 couts][8] fp16 = W[cout][8q + j][ky][kx]."""
+    if not conv64_eligible(c):
+        raise RuntimeError("conv64_weights: a 3x3 / stride 1 / pad 1, 64 -> 64 convolution required")
+    w = c.weight.detach().float().reshape(64, 8, 8, 3, 3).permute(3, 4, 1, 0, 2)   # [ky, kx, q, cout, j]
+    return w.reshape(9, 8, 64, 8).contiguous().half()
+
+
+def conv64(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, act: str = "relu",
+           res: torch.Tensor | None = None) -> torch.Tensor:
+    """``act(conv(x) + bias (+ res))`` for layer1's 64 -> 64 3x3 convolutions
+    in one fp16 matrix-core pass (``pv_conv64_f16``): x / res [n, 64, h, w]
+    channels_last float16 CUDA, ``w`` from :func:`conv64_weights`."""
+    n, c, h, wd = x.shape
+    cl = torch.channels_last
+    if x.dtype != torch.float16 or not x.is_cuda or c != 64 or not x.is_contiguous(memory_format=cl):
+        raise RuntimeError("conv64: a [n, 64, h, w] channels_last float16 CUDA map required")
+    if res is not None and (tuple(res.shape) != tuple(x.shape) or not res.is_contiguous(memory_format=cl)):
+        raise RuntimeError("conv64: residual [n, 64, h, w] channels_last required")
+    if act not in ("none", "relu"):
+        raise RuntimeError("conv64: act none or relu")
+    out = torch.empty_like(x, memory_format=cl)
+    _dev_call("pv_conv64_f16", None, x, x.data_ptr(), w.data_ptr(), bias.data_ptr(),
+              None if res is None else res.data_ptr(), out.data_ptr(), n, h, wd, _ACT[act])
+    return out
+
+
 def conv3x3_eligible(c: nn.Conv2d) -> bool:
     """The convolutions ``pv_conv3x3_f16`` takes: 3x3, stride 1, padding =
     dilation, no groups, Cin a multiple of 64, Cout of 128 (layer2's stride-1
@@ -501,20 +536,27 @@ class PVNetInference(nn.Module):
                            and self.conv2s[0].out_channels == 32)
         self.eval()
 
-    def _wide(self, c: nn.Conv2d, x):
-        """fp16 and a wide 3x3 convolution (layer3, layer4, fc): the weight for
-        pv_conv3x3_f16, made once; else None (MIOpen + pv_conv_epilogue)."""
-        if not (self.fused_conv and x.dtype == torch.float16 and conv3x3_eligible(c)):
+    def _wide(self, c: nn.Conv2d, x, kind="wide"):
+        """fp16 and a 3x3 convolution one of the matrix-core kernels takes
+        (kind "wide": pv_conv3x3_f16 -- layer2 / layer3 / layer4 / fc /
+        conv8s; "c64": pv_conv64_f16 -- layer1): its weight in that kernel's
+        layout, made once; else None (MIOpen + pv_conv_epilogue)."""
+        ok = conv3x3_eligible(c) if kind == "wide" else conv64_eligible(c)
+        if not (self.fused_conv and x.dtype == torch.float16 and ok):
             return None
-        key = (c.weight.data_ptr(), c.weight.dtype, c.weight._version)
+        key = (c.weight.data_ptr(), c.weight.dtype, c.weight._version, kind)
         cache = self.__dict__.setdefault("_wide_w", {})
         hit = cache.get(id(c))
         if hit is None or hit[0] != key:
-            hit = (key, conv3x3_weight(c))
+            hit = (key, conv3x3_weight(c) if kind == "wide" else conv64_weights(c))
             cache[id(c)] = hit
         return hit[1]
 
     def _conv_act(self, c: nn.Conv2d, x, act, res=None, rbias=None):
+        if rbias is None and act in ("none", "relu"):
+            w = self._wide(c, x, "c64")
+            if w is not None:
+                return conv64(x, w, c.bias, act, res=res)
         w = self._wide(c, x)
         if w is not None:
             return conv3x3(x, w, c.bias, c.dilation[0], act, res=res, rbias=rbias)

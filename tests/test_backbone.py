@@ -677,3 +677,53 @@ def test_stem_conv_matches_torch(hw, device):
     assert float(d.max()) <= 2 ** -7 * sc
     assert float(d.mean()) <= 2 ** -12 * sc
     assert pool.is_contiguous(memory_format=cl) and torch.equal(pool, F.max_pool2d(got, 3, 2, 1))
+
+
+def test_conv64_weight_layout():
+    """pv_conv64_f16's weight image (network.conv64_weights) follows
+    include/pvvote.h's formula W[cout][8q + j][ky][kx] (CPU)."""
+    from pvnet_amd.network import conv64_weights
+    g = torch.Generator().manual_seed(3)
+    c = torch.nn.Conv2d(64, 64, 3, 1, 1)
+    with torch.no_grad():
+        c.weight.copy_(torch.randn(64, 64, 3, 3, generator=g))
+    w = conv64_weights(c)
+    W = c.weight.detach().half()
+    for tap in range(9):
+        for q in range(8):
+            assert torch.equal(w[tap, q], W[:, 8 * q: 8 * q + 8, tap // 3, tap % 3])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["relu_120x160", "res_120x160", "none_ragged_13x37"])
+def test_conv64_matches_torch(case, device):
+    """pv_conv64_f16 (layer1's 64 -> 64 3x3 convolutions with bias, residual
+    and ReLU, RN:21-70) against MIOpen's fp16 convolution + ATen's bias /
+    residual / ReLU; tolerance as the conv3x3 test; ragged tiles included."""
+    from pvnet_amd.network import conv64, conv64_weights
+    F = torch.nn.functional
+    kind, hw = case.split("_")[0], case.split("_")[-1]
+    h, w = (int(v) for v in hw.split("x"))
+    g = torch.Generator().manual_seed(h * w)
+    cl = torch.channels_last
+    x = torch.randn(2, 64, h, w, generator=g).to(device, torch.float16).contiguous(memory_format=cl)
+    res = torch.randn(2, 64, h, w, generator=g).to(device, torch.float16).contiguous(memory_format=cl)
+    c = torch.nn.Conv2d(64, 64, 3, 1, 1).to(device)
+    with torch.no_grad():
+        c.weight.copy_(torch.randn(64, 64, 3, 3, generator=g) / 24)
+        c.bias.copy_(torch.randn(64, generator=g) * 0.5)
+    c = c.half()
+    with torch.no_grad():
+        y = F.conv2d(x, c.weight, None, 1, 1) + c.bias.view(1, -1, 1, 1)
+        if kind == "res":
+            y = y + res
+        ref = y if kind == "none" else torch.relu(y)
+        got = conv64(x, conv64_weights(c), c.bias, "none" if kind == "none" else "relu",
+                     res=res if kind == "res" else None)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape and got.is_contiguous(memory_format=cl)
+    sc = float(ref.abs().max())
+    d = (got.float() - ref.float()).abs()
+    print(f"conv64 {case}: max dev {float(d.max()):.3e}, mean {float(d.mean()):.2e} (scale {sc:.2f})")
+    assert float(d.max()) <= 2 ** -8 * sc
+    assert float(d.mean()) <= 2 ** -13 * sc
