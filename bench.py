@@ -616,11 +616,13 @@ def measure_e2e(dev, half=False, batch=1, iters=30, hn=512, form=None):
                 backbone_frac_of_matrix_peak=round(bb_tf / peak, 4),
                 voting_ms_per_batch=round((dt - dtb) * 1e3, 4), foreground_px=[int(tn.min()), int(tn.max())],
                 note="random-init weights (none ship with the reference): timing only; images/s covers backbone + "
-                     "v3 in one graph; backbone_form inference = pvnet_amd.network.PVNetInference (BN folded; MIOpen "
-                     "convolutions, each followed by one HIP epilogue pass for bias / residual / activation / the cat "
-                     "after fc; HIP upsample+cat; fp16: the decoder tail up2 + cat([fm, x]) + convraw (3x3 conv, "
-                     "LeakyReLU, 1x1 conv) as one matrix-core kernel, pv_decoder_tail_f16; f32: convraw's LeakyReLU "
-                     "+ 1x1 conv as one matrix-core pass); the backbone alone is a separate graph")
+                     "v3 in one graph; backbone_form inference = pvnet_amd.network.PVNetInference (BN folded). fp16: "
+                     "every convolution is a HIP matrix-core kernel with its epilogue fused (stem 7x7/2 as an s2d "
+                     "4x4 conv, layer1 halo kernel, layer2-4 / fc / conv8s implicit GEMM with the downsample 1x1 "
+                     "summed into conv2 and conv8s reading [xfc, x8s] from the two maps, the decoder's up2 + cat + "
+                     "conv steps and convraw + 1x1 head; DESIGN.md 7a); f32: MIOpen convolutions + one HIP epilogue "
+                     "pass each, HIP upsample+cat, convraw's LeakyReLU + 1x1 conv as one matrix-core pass; the "
+                     "backbone alone is a separate graph")
 
 
 def measure_kp_vs_ref(dev):

@@ -286,6 +286,34 @@ int pv_conv3x3_f16(const void *x, const void *w, const void *bias, const void *r
                    int32_t ldo, int32_t n, int32_t h, int32_t wd, int32_t cin, int32_t cout, int32_t dil,
                    int32_t act, float slope, pv_stream_t stream);
 
+/* pv_conv3x3_f16 generalised to the rest of the backbone's 3x3 convolutions (lib/networks/resnet.py:
+ * 21-70 BasicBlock with its downsample, :167-198 layer2's stride-2 first block; model_repository.py:
+ * 22-35,66 fc -> torch.cat([xfc, x8s], 1) -> conv8s):
+ *   x [n][hin][win][cin] read at stride `stride` (1 or 2; padding = dilation, so h = (hin - 1) / stride
+ *   + 1, wd likewise);
+ *   mode2 PV_CONV_X2_CAT: x2 [n][hin][win][cin2] is the concatenation's second part -- the 3x3
+ *   convolution runs over cat([x, x2]) (w [cout][3][3][cin + cin2]) without the concatenated map;
+ *   mode2 PV_CONV_X2_1X1: x2 [n][h2][w2][cin2] feeds a 1x1 convolution at stride s2 summed into the
+ *   same accumulator (the BasicBlock's downsample, its weight appended: w [cout][9 cin + cin2]);
+ *   rbias (its bias, res NULL) is added after the bias, before the activation.
+ * ws (256-byte aligned, ws_bytes from pv_conv3x3_workspace_bytes(n h wd, cout, K-steps), or NULL): the
+ * scratch that lets the launch cut its last partial round of 256-pixel tiles (tiles mod CUs) into K
+ * parts run side by side, the last-arriving part summing the others' f32 partials in part order (the
+ * result does not depend on the arrival order); K-steps = 9 (cin + cin2 for PV_CONV_X2_CAT) / 64
+ * (+ cin2 / 64 for PV_CONV_X2_1X1).  ws must be zero-filled before its first use; every call leaves
+ * it so.  One ws per stream at a time.
+ * Other arguments, alignment and roundings as pv_conv3x3_f16 (which is this with stride 1,
+ * PV_CONV_X2_NONE and no ws). */
+#define PV_CONV_X2_NONE 0
+#define PV_CONV_X2_CAT 1
+#define PV_CONV_X2_1X1 2
+int pv_conv3x3_ex_f16(const void *x, int32_t hin, int32_t win, int32_t stride, const void *x2, int32_t mode2,
+                      int32_t cin2, int32_t h2, int32_t w2, int32_t s2, const void *w, const void *bias,
+                      const void *res, const void *rbias, void *out, int32_t ldo, int32_t n, int32_t h,
+                      int32_t wd, int32_t cin, int32_t cout, int32_t dil, int32_t act, float slope, void *ws,
+                      int64_t ws_bytes, pv_stream_t stream);
+int64_t pv_conv3x3_workspace_bytes(int64_t pixels, int32_t cout, int32_t ksteps);
+
 /* replaces the decoder's half-resolution step (model_repository.py:43-51,75-78: up4sto2s, torch.cat([fm,
  * x2s], 1), conv2s = 3x3 conv + BN + LeakyReLU(slope)) in one fp16 matrix-core pass: fm [n][hin][win][64]
  * (conv4s's output), skip [n][2hin][2win][64] (x2s), out [n][2hin][2win][32], all channels-last.  w: the

@@ -84,6 +84,10 @@ SIGNATURES = [
     ("pv_relu_maxpool_f32", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp]),
     ("pv_conv3x3_f16", ctypes.c_int,
      [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_f32, c_vp]),
+    ("pv_conv3x3_ex_f16", ctypes.c_int,
+     [c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32,
+      c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_f32, c_vp, c_i64, c_vp]),
+    ("pv_conv3x3_workspace_bytes", c_i64, [c_i64, c_i32, c_i32]),
     ("pv_decoder_conv2s_f16", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp]),
     ("pv_decoder_conv4s_f16", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp]),
     ("pv_stem_conv_f16", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp]),

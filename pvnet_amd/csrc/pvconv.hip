@@ -413,15 +413,21 @@ constexpr int kCT = 256;                   // couts per tile (128 for Cout a mul
 constexpr int kPT = 256;                   // pixels per tile
 
 struct ConvArgs {
-    const _Float16 *x;      // [N][H][W][Cin]
-    const _Float16 *w;      // [Cout][9][Cin]
+    const _Float16 *x;      // [N][Hin][Win][Cin]
+    const _Float16 *x2;     // second input or null: [N][H][W][Cin2] (cat) or [N][H2][W2][Cin2] (1x1)
+    const _Float16 *w;      // [Cout][ksteps][64]: tap-major [9][Cin (+ Cin2)], then (1x1) [Cin2]
     const _Float16 *bias;   // [Cout]
     const _Float16 *res;    // [N][H][W][Cout] or null
     const _Float16 *rbias;  // [Cout] or null
-    _Float16 *out;          // [N][H][W][Cout]
+    _Float16 *out;          // [N][H][W][ldo]
     int N, H, W, Cin, Cout, ldo, dil, act, ntp, nct, ntiles, ksteps, cblocks;
+    int Hin, Win, stride;   // the main input's geometry (output pixel (y, x) reads (stride y + dy, stride x + dx))
+    int mode2, Cin2, H2, W2, s2, cb1, nmain;   // PV_CONV_X2_*; cb1 = Cin / 64; nmain = 9 cblocks
+    int nfull, nsplit;      // tiles run whole (blocks 0 .. nfull-1); each later tile in nsplit K parts
+    u4 *slab;               // split tiles' f32 partials [tail][part][f][1024 threads] (16 B each)
+    int *tick;              // [tail] arrival counters (zeroed per call)
     float slope;
-    int64_t M;              // pixels
+    int64_t M;              // output pixels
 };
 
 // LDS image of a stage: row r's 16-byte segment s at granule 8 r + (s ^ (r & 7))
@@ -452,24 +458,37 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
     const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
     // XCD-aware tile order: blocks i, i + 8, ... share an XCD; give each XCD a
     // contiguous range of tiles, cout tile major
-    int bid = (int)blockIdx.x;
-    {
-        const int nb = (int)gridDim.x, q = nb / 8, r = nb % 8, x = bid % 8;
+    // The last partial round of tiles (ntiles mod CUs) is cut into nsplit K
+    // parts run by nsplit blocks each (dispatched last), so that round ends
+    // nsplit x sooner; the part that arrives last sums the others' f32
+    // partials (in part order: deterministic) and runs the epilogue.
+    int bid = (int)blockIdx.x, part = 0, tail = -1;
+    if (bid < a.nfull) {
+        const int nb = a.nfull, q = nb / 8, r = nb % 8, x = bid % 8;
         bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+    } else {
+        const int j = bid - a.nfull;
+        tail = j / a.nsplit;
+        part = j - tail * a.nsplit;
+        bid = a.nfull + tail;
     }
     const int ct = bid / a.ntp, pt = bid % a.ntp;
     const int n0 = ct * CT;
     const int64_t p0 = (int64_t)pt * kPT;
     const __amdgpu_buffer_rsrc_t wr =
-        __builtin_amdgcn_make_buffer_rsrc((void *)a.w, 0, (int)((int64_t)a.Cout * 9 * a.Cin * 2), 0x00020000);
-    const __amdgpu_buffer_rsrc_t xr =
-        __builtin_amdgcn_make_buffer_rsrc((void *)a.x, 0, (int)(a.M * a.Cin * 2), 0x00020000);
-    const int K2 = 9 * a.Cin * 2;            // bytes per weight row
-    const int cbk = a.Cin / KB;              // channel blocks per tap
-    const int ksteps = 9 * cbk;
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.w, 0, (int)((int64_t)a.Cout * a.ksteps * 128), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)a.x, 0, (int)((int64_t)a.N * a.Hin * a.Win * a.Cin * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t x2r = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)a.x2, 0,
+        a.mode2 == PV_CONV_X2_1X1 ? (int)((int64_t)a.N * a.H2 * a.W2 * a.Cin2 * 2)
+                                  : (int)((int64_t)a.N * a.Hin * a.Win * a.Cin2 * 2),
+        0x00020000);
+    const int K2 = a.ksteps * RB;            // bytes per weight row
+    const int cbk = a.cblocks;               // channel blocks per tap (both inputs' for a cat)
+    const int ksteps = a.ksteps;
     // this lane's NW weight and NI pixel granules per stage: granule g = (N wid + i) 64 + lane
-    int woff[NW], py[NI], px[NI];
-    int64_t pbase[NI];
+    int woff[NW], py[NI], px[NI], iy[NI], sg16[NI];
     bool pin[NI];
 #pragma unroll
     for (int i = 0; i < NW; ++i) {
@@ -487,25 +506,44 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
         const int img = (int)(pc / ((int64_t)a.H * a.W)), rem = (int)(pc - (int64_t)img * a.H * a.W);
         py[i] = rem / a.W;
         px[i] = rem - py[i] * a.W;
-        pbase[i] = pc * a.Cin * 2 + seg * 16;
+        iy[i] = img;
+        sg16[i] = seg * 16;
     }
     auto issue_w = [&](int s, int buf) {
-        const int tap = s / cbk, cb = s - tap * cbk;
         uint8_t *st = lds + buf * STAGE;
 #pragma unroll
-        for (int i = 0; i < NW; ++i)
-            glds16(wr, st + (NW * wid + i) * 1024, woff[i], (tap * a.Cin + cb * KB) * 2);
+        for (int i = 0; i < NW; ++i) glds16(wr, st + (NW * wid + i) * 1024, woff[i], s * RB);
     };
     auto issue_x = [&](int s, int buf) {
+        uint8_t *st = lds + buf * STAGE + CT * RB;
+        if (a.mode2 == PV_CONV_X2_1X1 && s >= a.nmain) {
+            // the 1x1 second input (the BasicBlock's downsample): centre tap at stride s2
+            const int cbo = (s - a.nmain) * RB;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const int q = (iy[i] * a.H2 + py[i] * a.s2) * a.W2 + px[i] * a.s2;
+                const uint32_t off = pin[i] ? (uint32_t)(q * a.Cin2 * 2 + cbo + sg16[i]) : 0x80000000u;
+                glds16(x2r, st + (NI * wid + i) * 1024, off, 0);
+            }
+            return;
+        }
         const int tap = s / cbk, cb = s - tap * cbk;
         const int dy = (tap / 3 - 1) * a.dil, dx = (tap % 3 - 1) * a.dil;
-        uint8_t *st = lds + buf * STAGE;
-        const int dpix = (dy * a.W + dx) * a.Cin * 2 + cb * RB;
+        const bool second = a.mode2 == PV_CONV_X2_CAT && cb >= a.cb1;   // the concatenation's second part
+        const int C = second ? a.Cin2 : a.Cin, cbo = (second ? cb - a.cb1 : cb) * RB;
+        uint32_t off[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            const bool ok = pin[i] && (unsigned)(py[i] + dy) < (unsigned)a.H && (unsigned)(px[i] + dx) < (unsigned)a.W;
-            const uint32_t off = ok ? (uint32_t)(pbase[i] + dpix) : 0x80000000u;
-            glds16(xr, st + CT * RB + (NI * wid + i) * 1024, off, 0);
+            const int y = py[i] * a.stride + dy, x = px[i] * a.stride + dx;
+            const bool ok = pin[i] && (unsigned)y < (unsigned)a.Hin && (unsigned)x < (unsigned)a.Win;
+            off[i] = ok ? (uint32_t)(((iy[i] * a.Hin + y) * a.Win + x) * C * 2 + cbo + sg16[i]) : 0x80000000u;
+        }
+        if (second) {
+#pragma unroll
+            for (int i = 0; i < NI; ++i) glds16(x2r, st + (NI * wid + i) * 1024, off[i], 0);
+        } else {
+#pragma unroll
+            for (int i = 0; i < NI; ++i) glds16(xr, st + (NI * wid + i) * 1024, off[i], 0);
         }
     };
     auto issue = [&](int s, int buf) { issue_w(s, buf); issue_x(s, buf); };
@@ -542,19 +580,64 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
 #endif
         }
     };
-    issue(0, 0);
-    for (int s = 0; s < ksteps; ++s) {
-        const int buf = s & 1;
+    const int k0 = tail < 0 ? 0 : part * ksteps / a.nsplit;
+    const int k1 = tail < 0 ? ksteps : (part + 1) * ksteps / a.nsplit;
+    issue(k0, 0);
+    for (int s = k0; s < k1; ++s) {
+        const int buf = (s - k0) & 1;
         __builtin_amdgcn_s_waitcnt(0x0F70);          // this wave's loads of step s have landed (vmcnt 0)
         __syncthreads();                              // ... and every wave's; step s-1's reads are done
 #ifdef PVC_NO_LOADS
-        const bool nx = s == 0 && ksteps > 1;
+        const bool nx = s == k0 && k1 - k0 > 1;
 #else
-        const bool nx = s + 1 < ksteps;
+        const bool nx = s + 1 < k1;
 #endif
         if (nx) issue(s + 1, buf ^ 1);
         compute_kc(lds + buf * STAGE, 0);
         compute_kc(lds + buf * STAGE, 1);
+    }
+    if (tail >= 0) {
+        // Hand-off (MI355X_MICROARCH.md, "Valid forms", sc1 row): sc1
+        // (write-through) partial stores, every wave's vmcnt(0), a barrier,
+        // one agent-scope ticket add; the last arriver reads every other
+        // part's partials with sc1 loads.
+        constexpr int NF = MI * 4;                    // 16-byte accumulator groups per thread
+        const int64_t slab_bytes = (int64_t)a.nsplit * NF * (64 * kNW) * 16;
+        const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)((uint8_t *)a.slab + (int64_t)tail * slab_bytes), 0, (int)slab_bytes, 0x00020000);
+        const int tbase = (int)threadIdx.x * 16;
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+                const int f = mi * 4 + ni;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, acc[mi][ni]), sr,
+                                                       ((part * NF + f) * (64 * kNW)) * 16 + tbase, 0, 16);
+            }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int *flag = (int *)lds;                       // the stages are free: the loop's reads are done
+        if (threadIdx.x == 0) {
+            const int t = __hip_atomic_fetch_add(&a.tick[tail], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            flag[0] = t == a.nsplit - 1;
+        }
+        __syncthreads();
+        if (!flag[0]) return;
+        if (threadIdx.x == 0) a.tick[tail] = 0;       // zero again for the next call on this ws
+        // every part's partials from the slabs (this block's own included), in
+        // part order: the sum does not depend on which part arrived last, and
+        // the accumulators are reused (no second register set)
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+                const int f = mi * 4 + ni;
+                f4v t = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(sr, f * (64 * kNW) * 16 + tbase, 0, 16));
+                for (int p = 1; p < a.nsplit; ++p)
+                    t += __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     sr, ((p * NF + f) * (64 * kNW)) * 16 + tbase, 0, 16));
+                acc[mi][ni] = t;
+            }
     }
     // ---- epilogue: lane's accumulator (mi, ni) = couts c .. c+3 of pixel p;
     // k_epilogue's roundings (bias add, residual (+ its bias), activation) ----
@@ -590,6 +673,10 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
                 }
 #pragma unroll
                 for (int j = 0; j < 4; ++j) y[j] = (_Float16)((float)y[j] + (float)rr[j]);
+            } else if (a.rbias) {
+                // the downsample's bias (its convolution summed in the accumulator)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) y[j] = (_Float16)((float)y[j] + (float)rbq[mi][j]);
             }
             if (a.act == 1) {
 #pragma unroll
@@ -1149,35 +1236,106 @@ extern "C" int pv_decoder_tail_f16(const void *fm, const void *img, const void *
 extern "C" void pv_debug_set_tail_trace(void *p) { g_tail_trace = (unsigned long long *)p; }
 #endif
 
-extern "C" int pv_conv3x3_f16(const void *x, const void *w, const void *bias, const void *res, const void *rbias,
-                              void *out, int32_t ldo, int32_t n, int32_t h, int32_t wd, int32_t cin, int32_t cout,
-                              int32_t dil, int32_t act, float slope, pv_stream_t stream) {
+namespace {
+// The split of the last partial round (k_conv3x3): tiles run whole, parts per
+// later tile, and the workspace it needs (counters, then the f32 partials).
+struct ConvSplit {
+    int nfull, nsplit;
+    int64_t tick_bytes, bytes;
+};
+ConvSplit conv_split(int64_t pixels, int32_t cout, int32_t ksteps) {
+    const bool wide = cout % kCT == 0;
+    const int64_t ntiles = (pixels + kPT - 1) / kPT * (cout / (wide ? kCT : 128));
+    const int cus = cu_count_dec();
+    const int64_t rem = ntiles % cus;
+    int S = rem > 0 ? (int)std::min<int64_t>(4, cus / rem) : 1;
+    while (S > 1 && ksteps / S < 4) --S;          // parts of at least 4 K-steps
+    if (S < 2) return ConvSplit{(int)ntiles, 1, 0, 0};
+    const int64_t tb = (rem * 4 + 255) / 256 * 256;
+    const int64_t per = (int64_t)S * (wide ? 16 : 8) * (64 * kNW) * 16;   // one tile's partials
+    return ConvSplit{(int)(ntiles - rem), S, tb, tb + rem * per};
+}
+}  // namespace
+
+extern "C" int64_t pv_conv3x3_workspace_bytes(int64_t pixels, int32_t cout, int32_t ksteps) {
+    if (pixels <= 0 || cout <= 0 || cout % 128 || ksteps <= 0) return 0;
+    return conv_split(pixels, cout, ksteps).bytes;
+}
+
+extern "C" int pv_conv3x3_ex_f16(const void *x, int32_t hin, int32_t win, int32_t stride, const void *x2,
+                                 int32_t mode2, int32_t cin2, int32_t h2, int32_t w2, int32_t s2, const void *w,
+                                 const void *bias, const void *res, const void *rbias, void *out, int32_t ldo,
+                                 int32_t n, int32_t h, int32_t wd, int32_t cin, int32_t cout, int32_t dil, int32_t act,
+                                 float slope, void *ws, int64_t ws_bytes, pv_stream_t stream) {
     if (!x || !w || !bias || !out || n < 0 || h <= 0 || wd <= 0 || dil < 1 || act < 0 || act > 2) return PV_EINVAL;
-    if (cin <= 0 || cin % 64 || cout <= 0 || cout % 128 || (rbias && !res)) return PV_EINVAL;
+    if (cin <= 0 || cin % 64 || cout <= 0 || cout % 128 || (rbias && !res && mode2 != PV_CONV_X2_1X1))
+        return PV_EINVAL;
+    if (stride != 1 && stride != 2) return PV_EINVAL;
+    // the output's geometry is the convolution's: padding = dilation, kernel 3
+    if (hin <= 0 || win <= 0 || h != (hin - 1) / stride + 1 || wd != (win - 1) / stride + 1) return PV_EINVAL;
+    if (mode2 != PV_CONV_X2_NONE && mode2 != PV_CONV_X2_CAT && mode2 != PV_CONV_X2_1X1) return PV_EINVAL;
+    if (mode2 != PV_CONV_X2_NONE && (!x2 || cin2 <= 0 || cin2 % 64 || ((uintptr_t)x2 % 16))) return PV_EINVAL;
+    if (mode2 == PV_CONV_X2_1X1 && (s2 < 1 || h2 <= 0 || w2 <= 0 || (int64_t)(h - 1) * s2 >= h2 ||
+                                    (int64_t)(wd - 1) * s2 >= w2 || res))
+        return PV_EINVAL;
     if (ldo == 0) ldo = cout;
     if (ldo < cout || ldo % 4) return PV_EINVAL;
     if (((uintptr_t)x | (uintptr_t)w | (uintptr_t)out | (uintptr_t)res) % 16 || ((uintptr_t)bias | (uintptr_t)rbias) % 8)
         return PV_EALIGN;
-    if (out == x || (res && out == res)) return PV_EINVAL;
+    if (out == x || (res && out == res) || (x2 && out == x2)) return PV_EINVAL;
     if (n == 0) return PV_OK;
     ConvArgs a;
     a.x = (const _Float16 *)x; a.w = (const _Float16 *)w; a.bias = (const _Float16 *)bias;
+    a.x2 = mode2 != PV_CONV_X2_NONE ? (const _Float16 *)x2 : (const _Float16 *)x;
     a.res = (const _Float16 *)res; a.rbias = (const _Float16 *)rbias; a.out = (_Float16 *)out;
     a.N = n; a.H = h; a.W = wd; a.Cin = cin; a.Cout = cout; a.ldo = ldo; a.dil = dil; a.act = act; a.slope = slope;
+    a.Hin = hin; a.Win = win; a.stride = stride;
+    a.mode2 = mode2; a.Cin2 = mode2 != PV_CONV_X2_NONE ? cin2 : 0; a.H2 = h2; a.W2 = w2; a.s2 = s2;
     a.M = (int64_t)n * h * wd;
+    a.cb1 = cin / 64;
+    a.cblocks = (cin + (mode2 == PV_CONV_X2_CAT ? cin2 : 0)) / 64;
+    a.nmain = 9 * a.cblocks;
+    a.ksteps = a.nmain + (mode2 == PV_CONV_X2_1X1 ? cin2 / 64 : 0);
     // 32-bit buffer offsets (+ the 0x80000000 out-of-range marker): the maps under 2 GiB
-    if (a.M * cin * 2 >= (1ll << 31) || (int64_t)cout * 9 * cin * 2 >= (1ll << 31) || a.M * ldo >= (1ll << 31))
+    const int64_t in1 = (int64_t)n * hin * win * cin * 2;
+    const int64_t in2 = mode2 == PV_CONV_X2_1X1 ? (int64_t)n * h2 * w2 * cin2 * 2
+                        : mode2 == PV_CONV_X2_CAT ? (int64_t)n * hin * win * cin2 * 2 : 0;
+    if (in1 >= (1ll << 31) || in2 >= (1ll << 31) || (int64_t)cout * a.ksteps * 128 >= (1ll << 31) ||
+        a.M * ldo >= (1ll << 31))
         return PV_EINVAL;
-    a.cblocks = cin / 64;
-    a.ksteps = 9 * a.cblocks;
     a.ntp = (int)((a.M + kPT - 1) / kPT);
     const bool wide = cout % kCT == 0;       // 256-cout tiles, else 128
     a.nct = cout / (wide ? kCT : 128);
     a.ntiles = a.ntp * a.nct;
-    if (wide) k_conv3x3<kCT><<<(unsigned)a.ntiles, 64 * kNW, 0, (hipStream_t)stream>>>(a);
-    else k_conv3x3<128><<<(unsigned)a.ntiles, 64 * kNW, 0, (hipStream_t)stream>>>(a);
+    a.nfull = a.ntiles;
+    a.nsplit = 1;
+    a.slab = nullptr;
+    a.tick = nullptr;
+    if (ws) {
+        if ((uintptr_t)ws % 256) return PV_EALIGN;
+        const ConvSplit sp = conv_split(a.M, cout, a.ksteps);
+        if (sp.nsplit > 1 && ws_bytes >= sp.bytes) {
+            a.nfull = sp.nfull;
+            a.nsplit = sp.nsplit;
+            // the counters start zeroed (the caller's zero-filled ws) and every
+            // split tile's last part returns its counter to zero: no memset node
+            a.tick = (int *)ws;
+            a.slab = (u4 *)((uint8_t *)ws + sp.tick_bytes);
+        }
+    }
+    const unsigned grid = (unsigned)(a.nfull + (a.ntiles - a.nfull) * a.nsplit);
+    if (wide) k_conv3x3<kCT><<<grid, 64 * kNW, 0, (hipStream_t)stream>>>(a);
+    else k_conv3x3<128><<<grid, 64 * kNW, 0, (hipStream_t)stream>>>(a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? PV_OK : (int)e;
+}
+
+extern "C" int pv_conv3x3_f16(const void *x, const void *w, const void *bias, const void *res, const void *rbias,
+                              void *out, int32_t ldo, int32_t n, int32_t h, int32_t wd, int32_t cin, int32_t cout,
+                              int32_t dil, int32_t act, float slope, pv_stream_t stream) {
+    if (rbias && !res) return PV_EINVAL;
+    return pv_conv3x3_ex_f16(x, h, wd, 1, nullptr, PV_CONV_X2_NONE, 0, 0, 0, 0, w, bias, res, rbias, out, ldo, n, h,
+                             wd, cin, cout, dil, act, slope, nullptr, 0, stream);
 }
 
 extern "C" int pv_decoder_conv2s_f16(const void *fm, const void *skip, const void *w, const void *bias, void *out,

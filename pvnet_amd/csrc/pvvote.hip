@@ -352,6 +352,9 @@ struct VertexView {
     int32_t extent;     // bytes spanned by one image's [h,w,vn,2] view (< 2^31: buffer-load range)
 };
 
+#ifndef PVV_COMPACT_SKIP
+#define PVV_COMPACT_SKIP 1   // k_compact blocks without foreground exit at once
+#endif
 constexpr int kCompactKp = 12;   // keypoints whose vertex loads a compaction thread keeps in flight at once
 constexpr uint64_t kLookbackSpin = 20000;   // s_memrealtime ticks (100 MHz): 200 us
 __device__ int g_lb_self;   // debug (pv_debug_lookback_self): every look-back count worked out by the waiter
@@ -368,6 +371,13 @@ __global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int 
     __shared__ int sh[8];
     __shared__ int wcnt[4];
     cstamp(blk, 0);
+#if PVV_COMPACT_SKIP
+    // a block without foreground has nothing to store; only blocks 0 and
+    // nblk - 1 (which write tn / fgtot) run on.  The downsampling look-back
+    // below takes such a predecessor's kept count as 0 from its k_fg_count
+    // count, without waiting for it.
+    if (blk != 0 && blk != nblk - 1 && blkcnt[b * nblk + blk] == 0) return;
+#endif
     // one round trip: this wave's foreground ballot (k_fg_count) beside the
     // image's per-block counts (the total and this block's row-major offset)
     const uint64_t fw = fgbits[((int64_t)b * nblk + blk) * 4 + wid];
@@ -442,6 +452,9 @@ __global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int 
         // so no thread waits longer than kLookbackSpin in all
         const uint64_t t_dead = __builtin_amdgcn_s_memrealtime() + kLookbackSpin;
         for (int j = threadIdx.x; j < blk; j += 256) {
+#if PVV_COMPACT_SKIP
+            if (blkcnt[b * nblk + j] == 0) continue;   // no foreground: kept 0 (the block may not publish)
+#endif
             int v = self_all ? 0 : ld_agent(&agg[j]);
             if (v == 0 && !self_all)
                 while ((v = ld_agent(&agg[j])) == 0 && __builtin_amdgcn_s_memrealtime() < t_dead)
@@ -3261,7 +3274,7 @@ const char *pv_build_config(void) {
            PVV_STR(PVV_VM_RW3_1) "/" PVV_STR(PVV_VM_RW3_2) ")"
            " hypgen=" PVV_STR(PVV_HYPGEN)
            " refine=" PVV_STR(PVV_REFINE_NJ) "x" PVV_STR(PVV_REFINE_T)
-           " fg_cpb=" PVV_STR(PVV_FG_CPB)
+           " fg_cpb=" PVV_STR(PVV_FG_CPB) " compact_skip=" PVV_STR(PVV_COMPACT_SKIP)
            " bytes=k_vote_bytes(rows=" PVV_STR(PVV_BYTE_HB) ",xcd=" PVV_STR(PVV_BYTES_XCD) ",bal=" PVV_STR(PVV_BYTES_BAL) ")"
 #ifdef PVV_TRACE
            " TRACE"

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import math
 
+
 import torch
 import torch.nn.functional as F
 from torch import nn
@@ -352,11 +353,24 @@ def conv64(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, act: str = "rel
 
 
 def conv3x3_eligible(c: nn.Conv2d) -> bool:
-    """The convolutions ``pv_conv3x3_f16`` takes: 3x3, stride 1, padding =
-    dilation, no groups, Cin a multiple of 64, Cout of 128 (layer2's stride-1
-    convolutions, layer3, layer4, fc, conv8s)."""
-    return (c.kernel_size == (3, 3) and c.stride == (1, 1) and c.groups == 1 and c.padding == c.dilation
-            and c.dilation[0] == c.dilation[1] and c.in_channels % 64 == 0 and c.out_channels % 128 == 0)
+    """The convolutions ``pv_conv3x3_ex_f16`` takes: 3x3, stride 1 or 2,
+    padding = dilation, no groups, Cin a multiple of 64, Cout of 128 (layer2
+    -- its stride-2 first convolution included --, layer3, layer4, fc,
+    conv8s)."""
+    return (c.kernel_size == (3, 3) and c.stride[0] == c.stride[1] and c.stride[0] in (1, 2) and c.groups == 1
+            and c.padding == c.dilation and c.dilation[0] == c.dilation[1] and c.in_channels % 64 == 0
+            and c.out_channels % 128 == 0)
+
+
+def downsample_eligible(ds) -> bool:
+    """A BasicBlock downsample ``pv_conv3x3_ex_f16`` sums into conv2's
+    accumulator (PV_CONV_X2_1X1): one 1x1 convolution (BN folded), no
+    padding, Cin a multiple of 64."""
+    if ds is None or not isinstance(ds[0], nn.Conv2d) or not all(isinstance(m, nn.Identity) for m in ds[1:]):
+        return False                  # (fold_batchnorm leaves the folded BN as an Identity)
+    d = ds[0]
+    return (d.kernel_size == (1, 1) and d.padding == (0, 0) and d.groups == 1 and d.stride[0] == d.stride[1]
+            and d.in_channels % 64 == 0 and d.bias is not None)
 
 
 def conv3x3(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, dil: int, act: str = "relu",
@@ -378,15 +392,76 @@ def conv3x3(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, dil: int, act:
     if res is not None and (tuple(res.shape) != (n, cout, h, wd) or not res.is_contiguous(memory_format=cl)):
         raise RuntimeError("conv3x3: residual [n, cout, h, w] channels_last required")
     out = torch.empty((n, cout + extra, h, wd), dtype=x.dtype, device=x.device, memory_format=cl)
-    _dev_call("pv_conv3x3_f16", None, x, x.data_ptr(), w.data_ptr(), bias.data_ptr(),
-              None if res is None else res.data_ptr(), None if rbias is None else rbias.data_ptr(), out.data_ptr(),
-              cout + extra, n, h, wd, cin, cout, int(dil), _ACT[act], float(slope))
+    ws, wsb = _conv_workspace(x, n * h * wd, cout, 9 * cin // 64)
+    _dev_call("pv_conv3x3_ex_f16", None, x, x.data_ptr(), h, wd, 1, None, 0, 0, 0, 0, 0, w.data_ptr(),
+              bias.data_ptr(), None if res is None else res.data_ptr(), None if rbias is None else rbias.data_ptr(),
+              out.data_ptr(), cout + extra, n, h, wd, cin, cout, int(dil), _ACT[act], float(slope), ws, wsb)
     return out
 
 
-def conv3x3_weight(c: nn.Conv2d) -> torch.Tensor:
-    """c's weight as pv_conv3x3_f16 reads it: [cout, 3, 3, cin], fp16, contiguous."""
-    return c.weight.detach().permute(0, 2, 3, 1).contiguous().half()
+_CONV_WS: dict = {}
+
+
+def _conv_workspace(x: torch.Tensor, pixels: int, cout: int, ksteps: int):
+    """The split-K scratch of pv_conv3x3_ex_f16 (its last partial round of
+    tiles): one buffer per (device, stream), since calls on one stream run in
+    order; grown to the largest need and kept, so a captured graph keeps
+    using the buffer it captured (a buffer first made during a capture comes
+    from the graph's pool).  (pointer, bytes) or (None, 0)."""
+    from pvnet_amd import _lib
+    need = int(_lib.load().pv_conv3x3_workspace_bytes(pixels, cout, ksteps))
+    if need <= 0:
+        return None, 0
+    key = (x.device, torch.cuda.current_stream(x.device).cuda_stream)
+    bufs = _CONV_WS.setdefault(key, [])
+    if not bufs or bufs[-1].numel() < need:
+        # a smaller buffer is kept alive too: a graph captured with it still uses it
+        bufs.append(torch.zeros(need, dtype=torch.uint8, device=x.device))   # zeroed once (pvvote.h)
+    return bufs[-1].data_ptr(), bufs[-1].numel()
+
+
+def conv3x3_weight(c: nn.Conv2d, ds: nn.Conv2d | None = None) -> torch.Tensor:
+    """c's weight as pv_conv3x3_f16 reads it: [cout, 3, 3, cin], fp16, contiguous;
+    with ``ds`` (a 1x1 downsample) [cout, 9 cin + cin_ds]: the 1x1 weights
+    appended to each output channel's row (pv_conv3x3_ex_f16, PV_CONV_X2_1X1)."""
+    w = c.weight.detach().permute(0, 2, 3, 1).contiguous().half()
+    if ds is None:
+        return w
+    wd = ds.weight.detach().reshape(ds.out_channels, ds.in_channels).half()
+    return torch.cat([w.reshape(c.out_channels, -1), wd], 1).contiguous()
+
+
+def conv3x3_ex(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, dil: int, stride: int = 1, act: str = "relu",
+               x2: torch.Tensor | None = None, mode2: str = "none", s2: int = 1, rbias: torch.Tensor | None = None,
+               res: torch.Tensor | None = None, slope: float = 0.1) -> torch.Tensor:
+    """``pv_conv3x3_ex_f16``: a 3x3 convolution of x at ``stride`` (padding =
+    dilation) and its epilogue, with an optional second input: ``mode2``
+    "cat" -- the convolution runs over ``torch.cat([x, x2], 1)`` (w [cout, 3,
+    3, cin + cin2]); "1x1" -- a 1x1 convolution of x2 at stride ``s2`` is
+    summed into the same accumulator (w [cout, 9 cin + cin2],
+    :func:`conv3x3_weight` with ``ds``), its bias ``rbias`` added after
+    ``bias``.  channels_last float16 CUDA maps."""
+    n, cin, hin, win = x.shape
+    cout = w.shape[0]
+    cl = torch.channels_last
+    h, wd = (hin - 1) // stride + 1, (win - 1) // stride + 1
+    m2 = {"none": 0, "cat": 1, "1x1": 2}[mode2]
+    for t in (x, x2, res):
+        if t is not None and (t.dtype != torch.float16 or not t.is_cuda or not t.is_contiguous(memory_format=cl)):
+            raise RuntimeError("conv3x3_ex: channels_last float16 CUDA maps required")
+    cin2, h2, w2 = (0, 0, 0) if x2 is None else (x2.shape[1], x2.shape[2], x2.shape[3])
+    if (m2 == 0) != (x2 is None) or (m2 == 1 and (h2, w2) != (hin, win)) or x2 is not None and x2.shape[0] != n:
+        raise RuntimeError("conv3x3_ex: second input does not match mode2")
+    k = 9 * (cin + (cin2 if m2 == 1 else 0)) + (cin2 if m2 == 2 else 0)
+    if w.dtype != torch.float16 or not w.is_contiguous() or w.numel() != cout * k:
+        raise RuntimeError("conv3x3_ex: weight [cout, K] contiguous float16 required")
+    out = torch.empty((n, cout, h, wd), dtype=x.dtype, device=x.device, memory_format=cl)
+    ws, wsb = _conv_workspace(x, n * h * wd, cout, k // 64)
+    _dev_call("pv_conv3x3_ex_f16", None, x, x.data_ptr(), hin, win, int(stride),
+              None if x2 is None else x2.data_ptr(), m2, cin2, h2, w2, int(s2), w.data_ptr(), bias.data_ptr(),
+              None if res is None else res.data_ptr(), None if rbias is None else rbias.data_ptr(), out.data_ptr(),
+              cout, n, h, wd, cin, cout, int(dil), _ACT[act], float(slope), ws, wsb)
+    return out
 
 
 def decoder_conv2s_weights(c: nn.Conv2d):
@@ -559,14 +634,37 @@ class PVNetInference(nn.Module):
                 return conv64(x, w, c.bias, act, res=res)
         w = self._wide(c, x)
         if w is not None:
+            if c.stride[0] != 1:
+                if res is not None:
+                    return conv_epilogue(_conv(x, c), c.bias, act, res=res, rbias=rbias)
+                return conv3x3_ex(x, w, c.bias, c.dilation[0], stride=c.stride[0], act=act)
             return conv3x3(x, w, c.bias, c.dilation[0], act, res=res, rbias=rbias)
         return conv_epilogue(_conv(x, c), c.bias, act, res=res, rbias=rbias)
+
+    def _conv_ds(self, c: nn.Conv2d, ds: nn.Conv2d, y, x):
+        """conv2 of a BasicBlock with a downsample: ReLU(conv2(y) + b2 +
+        ds(x) + bd) in one pv_conv3x3_ex_f16 pass (the 1x1 convolution
+        summed into conv2's accumulator; RN:41-70), or None."""
+        if not (self.fused_conv and y.dtype == torch.float16 and conv3x3_eligible(c) and c.stride == (1, 1)):
+            return None
+        key = (c.weight.data_ptr(), c.weight._version, ds.weight.data_ptr(), ds.weight._version, "ds")
+        cache = self.__dict__.setdefault("_wide_w", {})
+        hit = cache.get(id(c))
+        if hit is None or hit[0] != key:
+            hit = (key, conv3x3_weight(c, ds))
+            cache[id(c)] = hit
+        return conv3x3_ex(y, hit[1], c.bias, c.dilation[0], act="relu", x2=x, mode2="1x1", s2=ds.stride[0],
+                          rbias=ds.bias)
 
     def _block(self, blk: BasicBlock, x):
         y = self._conv_act(blk.conv1, x, "relu")
         if blk.downsample is None:
             res, rb = x, None
         else:
+            if downsample_eligible(blk.downsample):
+                out = self._conv_ds(blk.conv2, blk.downsample[0], y, x)
+                if out is not None:
+                    return out
             res, rb = _conv(x, blk.downsample[0]), blk.downsample[0].bias
         return self._conv_act(blk.conv2, y, "relu", res=res, rbias=rb)
 
@@ -608,13 +706,22 @@ class PVNetInference(nn.Module):
                 y = self._block(blk, y)
         # fc (conv + BN + ReLU, MR:22-26) and torch.cat([xfc, x8s], 1) (MR:66) in one epilogue
         wfc = self._wide(r.fc[0], y)
-        if wfc is not None:
+        c8 = self.conv8s[0]
+        w8 = self._wide(c8, y) if wfc is not None and c8.stride == (1, 1) else None
+        if w8 is not None and c8.in_channels == r.fc[0].out_channels + x8s.shape[1]:
+            # conv8s over torch.cat([xfc, x8s], 1) (MR:66) read from the two maps: no concatenated copy
             c = r.fc[0]
-            cat8 = conv3x3(y, wfc, c.bias, c.dilation[0], "relu", extra=x8s.shape[1])
-            cat8[:, c.out_channels:].copy_(x8s)
+            xfc = conv3x3(y, wfc, c.bias, c.dilation[0], "relu")
+            fm = conv3x3_ex(xfc, w8, c8.bias, c8.dilation[0], act="leaky", x2=x8s, mode2="cat",
+                            slope=self.conv8s[2].negative_slope)
         else:
-            cat8 = conv_epilogue(_conv(y, r.fc[0]), r.fc[0].bias, "relu", skip=x8s)
-        fm = self._conv_act(self.conv8s[0], cat8, "leaky")
+            if wfc is not None:
+                c = r.fc[0]
+                cat8 = conv3x3(y, wfc, c.bias, c.dilation[0], "relu", extra=x8s.shape[1])
+                cat8[:, c.out_channels:].copy_(x8s)
+            else:
+                cat8 = conv_epilogue(_conv(y, r.fc[0]), r.fc[0].bias, "relu", skip=x8s)
+            fm = self._conv_act(self.conv8s[0], cat8, "leaky")
         c4 = self.conv4s[0]
         if (fm.dtype == torch.float16 and self.fused_conv and fm.shape[1] == 128 and x4s.shape[1] == 64
                 and c4.in_channels == 192 and c4.out_channels == 64 and c4.kernel_size == (3, 3)):

@@ -488,7 +488,7 @@ def test_relu_maxpool_matches_torch(dtype, hw, device):
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["relu_128_256_d2", "res_256_256_d2", "resb_256_512_d4", "relu_512_512_d4",
                                   "fc_512_256_d1_ragged", "leaky_64_256_d1", "resb_128_128_d1",
-                                  "leaky_384_128_d1_ragged"])
+                                  "leaky_384_128_d1_ragged", "resb_256_512_d4_big", "relu_128_128_d1_big"])
 def test_conv3x3_matches_torch(case, device):
     """pv_conv3x3_f16 (the wide 3x3 convolutions of layer3 / layer4 / fc with
     their epilogue, RN:21-38 / MR:22-26) against MIOpen's fp16 convolution +
@@ -500,7 +500,8 @@ def test_conv3x3_matches_torch(case, device):
     from pvnet_amd.network import conv3x3, conv3x3_weight
     F = torch.nn.functional
     kind, cin, cout, d = case.split("_")[0], *[int(v) for v in case.split("_")[1:3]], int(case.split("_")[3][1:])
-    n, h, w = (3, 13, 17) if case.endswith("ragged") else (2, 30, 40)
+    # "big": more tiles than CUs, so whole tiles run beside the split last round
+    n, h, w = (3, 13, 17) if case.endswith("ragged") else (16, 60, 80) if case.endswith("big") else (2, 30, 40)
     g = torch.Generator().manual_seed(cin * 7 + cout + d)
     cl = torch.channels_last
     x = torch.randn(n, cin, h, w, generator=g).to(device, torch.float16).contiguous(memory_format=cl)
@@ -520,13 +521,99 @@ def test_conv3x3_matches_torch(case, device):
         ref = F.leaky_relu(y, 0.1) if act == "leaky" else torch.relu(y)
         got = conv3x3(x, conv3x3_weight(conv), conv.bias, d, act, res=res if use_res else None,
                       rbias=rb if use_rb else None)
+        again = conv3x3(x, conv3x3_weight(conv), conv.bias, d, act, res=res if use_res else None,
+                        rbias=rb if use_rb else None)
     torch.cuda.synchronize()
+    assert torch.equal(got, again)          # split tiles sum their parts in part order, whatever arrives last
     assert got.shape == ref.shape and got.is_contiguous(memory_format=cl)
     sc = float(ref.abs().max())
     dev_ = (got.float() - ref.float()).abs()
     print(f"conv3x3 {case}: max dev {float(dev_.max()):.3e}, mean {float(dev_.mean()):.2e} (scale {sc:.2f})")
     assert float(dev_.max()) <= 2 ** -8 * sc
     assert float(dev_.mean()) <= 2 ** -13 * sc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["s2_64_128_d1", "s2_64_128_d1_odd", "cat_256_128_d1", "cat_256_128_d1_ragged",
+                                  "ds1_128_256_d2", "ds2_64_128_d1", "ds2_64_128_d1_odd", "ds1_256_512_d4"])
+def test_conv3x3_ex_matches_torch(case, device):
+    """pv_conv3x3_ex_f16 against MIOpen's fp16 convolutions + ATen's epilogue
+    on the same inputs: "s2" layer2's stride-2 first convolution (RN:167-198);
+    "cat" conv8s over torch.cat([xfc, x8s], 1) read from the two maps (MR:66);
+    "ds1" / "ds2" a BasicBlock's conv2 with its 1x1 downsample (stride 1 / 2)
+    summed into the same accumulator, then bias, the downsample's bias and the
+    ReLU (RN:41-70).  Odd input sizes (stride 2) and a ragged pixel count
+    included.  Tolerance as test_conv3x3_matches_torch (the fused sum skips
+    the reference's fp16 roundings of the two convolutions)."""
+    from pvnet_amd.network import conv3x3_ex, conv3x3_weight
+    F = torch.nn.functional
+    parts = case.split("_")
+    kind, cin, cout, d = parts[0], int(parts[1]), int(parts[2]), int(parts[3][1:])
+    n, h, w = (3, 13, 17) if case.endswith("ragged") else (2, 31, 41) if case.endswith("odd") else (2, 30, 40)
+    g = torch.Generator().manual_seed(cin * 11 + cout + d + len(case))
+    cl = torch.channels_last
+
+    def rnd(*shape, scale=1.0):
+        return (torch.randn(*shape, generator=g) * scale).to(device, torch.float16)
+
+    def conv_w(co, ci, k):
+        return rnd(co, ci, k, k, scale=1.0 / (k * ci ** 0.5))
+
+    b = rnd(cout, scale=0.5)
+    with torch.no_grad():
+        if kind == "s2":
+            x = rnd(n, cin, h, w).contiguous(memory_format=cl)
+            wt = conv_w(cout, cin, 3)
+            ref = torch.relu(F.conv2d(x, wt, None, 2, d, d) + b.view(1, -1, 1, 1))
+            c = torch.nn.Conv2d(cin, cout, 3, 2, d, d).to(device).half()
+            c.weight.copy_(wt)
+            got = conv3x3_ex(x, conv3x3_weight(c), b, d, stride=2, act="relu")
+        elif kind == "cat":
+            c2 = 128
+            x = rnd(n, cin, h, w).contiguous(memory_format=cl)
+            x2 = rnd(n, c2, h, w).contiguous(memory_format=cl)
+            wt = conv_w(cout, cin + c2, 3)
+            ref = F.leaky_relu(F.conv2d(torch.cat([x, x2], 1), wt, None, 1, d, d) + b.view(1, -1, 1, 1), 0.1)
+            c = torch.nn.Conv2d(cin + c2, cout, 3, 1, d, d).to(device).half()
+            c.weight.copy_(wt)
+            got = conv3x3_ex(x, conv3x3_weight(c), b, d, act="leaky", x2=x2, mode2="cat")
+        else:
+            s2 = int(kind[2])
+            cmid = cout
+            xin = rnd(n, cin, h, w).contiguous(memory_format=cl)           # the block input
+            ho, wo = (h - 1) // s2 + 1, (w - 1) // s2 + 1
+            y = rnd(n, cmid, ho, wo).contiguous(memory_format=cl)          # conv1's output
+            wt = conv_w(cout, cmid, 3)
+            wd = conv_w(cout, cin, 1)
+            bd = rnd(cout, scale=0.5)
+            main = F.conv2d(y, wt, None, 1, d, d) + b.view(1, -1, 1, 1)
+            resid = F.conv2d(xin, wd, None, s2) + bd.view(1, -1, 1, 1)
+            ref = torch.relu(main + resid)
+            c = torch.nn.Conv2d(cmid, cout, 3, 1, d, d).to(device).half()
+            c.weight.copy_(wt)
+            ds = torch.nn.Conv2d(cin, cout, 1, s2).to(device).half()
+            ds.weight.copy_(wd)
+            got = conv3x3_ex(y, conv3x3_weight(c, ds), b, d, act="relu", x2=xin, mode2="1x1", s2=s2, rbias=bd)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape and got.is_contiguous(memory_format=cl)
+    sc = float(ref.abs().max())
+    dev_ = (got.float() - ref.float()).abs()
+    print(f"conv3x3_ex {case}: max dev {float(dev_.max()):.3e}, mean {float(dev_.mean()):.2e} (scale {sc:.2f})")
+    assert float(dev_.max()) <= 2 ** -8 * sc
+    assert float(dev_.mean()) <= 2 ** -13 * sc
+
+
+def test_conv3x3_weight_with_downsample():
+    """The PV_CONV_X2_1X1 weight rows: conv2's [cout][3][3][cmid] flattened,
+    then the 1x1 downsample's [cout][cin] (include/pvvote.h)."""
+    from pvnet_amd.network import conv3x3_weight
+    c = torch.nn.Conv2d(128, 256, 3, 1, 1)
+    ds = torch.nn.Conv2d(64, 256, 1, 2)
+    w = conv3x3_weight(c, ds).float()
+    assert tuple(w.shape) == (256, 9 * 128 + 64)
+    ref_main = c.weight.detach().permute(0, 2, 3, 1).reshape(256, -1).half().float()
+    assert torch.equal(w[:, :9 * 128], ref_main)
+    assert torch.equal(w[:, 9 * 128:], ds.weight.detach().reshape(256, 64).half().float())
 
 
 @pytest.mark.gpu
