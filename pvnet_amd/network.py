@@ -400,6 +400,7 @@ def conv3x3(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, dil: int, act:
 
 
 _CONV_WS: dict = {}
+CONV_SPLIT = True          # the split-K last round (A/B hook for tools/backbone_ab2.py; no environment switch)
 
 
 def _conv_workspace(x: torch.Tensor, pixels: int, cout: int, ksteps: int):
@@ -410,7 +411,7 @@ def _conv_workspace(x: torch.Tensor, pixels: int, cout: int, ksteps: int):
     from the graph's pool).  (pointer, bytes) or (None, 0)."""
     from pvnet_amd import _lib
     need = int(_lib.load().pv_conv3x3_workspace_bytes(pixels, cout, ksteps))
-    if need <= 0:
+    if need <= 0 or not CONV_SPLIT:
         return None, 0
     key = (x.device, torch.cuda.current_stream(x.device).cuda_stream)
     bufs = _CONV_WS.setdefault(key, [])
@@ -607,6 +608,9 @@ class PVNetInference(nn.Module):
         # when its shapes are the reference's (35 -> 32 -> 20 / 44); False = the MIOpen form
         # fp16: layer3 / layer4 / fc's 3x3 convolutions + epilogues as pv_conv3x3_f16
         self.fused_conv = True
+        # fp16: a BasicBlock's 1x1 downsample summed into its conv2 (pv_conv3x3_ex_f16), conv8s reading
+        # [xfc, x8s] from the two maps; False = the downsample as its own convolution + a residual read
+        self.fused_ds = True
         self.fused_tail = (c0.in_channels == 35 and c0.out_channels == 32 and f.convraw[3].out_channels in (20, 44)
                            and self.conv2s[0].out_channels == 32)
         self.eval()
@@ -661,7 +665,7 @@ class PVNetInference(nn.Module):
         if blk.downsample is None:
             res, rb = x, None
         else:
-            if downsample_eligible(blk.downsample):
+            if self.fused_ds and downsample_eligible(blk.downsample):
                 out = self._conv_ds(blk.conv2, blk.downsample[0], y, x)
                 if out is not None:
                     return out
@@ -707,7 +711,7 @@ class PVNetInference(nn.Module):
         # fc (conv + BN + ReLU, MR:22-26) and torch.cat([xfc, x8s], 1) (MR:66) in one epilogue
         wfc = self._wide(r.fc[0], y)
         c8 = self.conv8s[0]
-        w8 = self._wide(c8, y) if wfc is not None and c8.stride == (1, 1) else None
+        w8 = self._wide(c8, y) if wfc is not None and c8.stride == (1, 1) and self.fused_ds else None
         if w8 is not None and c8.in_channels == r.fc[0].out_channels + x8s.shape[1]:
             # conv8s over torch.cat([xfc, x8s], 1) (MR:66) read from the two maps: no concatenated copy
             c = r.fc[0]
