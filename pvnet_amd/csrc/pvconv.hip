@@ -38,6 +38,10 @@
 
 #include "../../include/pvvote.h"
 
+#ifndef PVC_L1_AHEAD
+#define PVC_L1_AHEAD 2      // halo kernels (k_conv64, k_dec_conv2s / 4s): fragment reads this many k-steps ahead of their MFMAs
+#endif
+
 namespace {
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -837,15 +841,23 @@ __global__ __launch_bounds__(512) void k_dec_conv2s(DecConvArgs a) {
         // ---- the convolution, part by part: wave = output row wid, 32 pixels ----
         f16x acc = {};
         auto conv_part = [&](int part) {
-#pragma unroll 4
-            for (int s = 0; s < 36; ++s) {
+            // fragments read PVC_L1_AHEAD k-steps ahead of their MFMAs (k_conv64)
+            auto frag = [&](int s, h8 &af, h8 &bf) {
                 const int o = 2 * s + h;                  // octet of this lane half: tap o / 8, channels 8 (o % 8)
                 const int tap = o >> 3, q = o & 7;
                 const int ky = tap / 3, kx = tap - 3 * ky;
-                const h8 af = *(const h8 *)(wl + ((part * 72 + o) * kDCo + n) * 16);
-                const int hp = (wid + ky) * kHC + n + kx;
-                const h8 bf = *(const h8 *)(halo + halo_granule(hp, q) * 16);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc, 0, 0, 0);
+                af = *(const h8 *)(wl + ((part * 72 + o) * kDCo + n) * 16);
+                bf = *(const h8 *)(halo + halo_granule((wid + ky) * kHC + n + kx, q) * 16);
+            };
+            constexpr int AH = PVC_L1_AHEAD;
+            h8 fa[AH + 1], fb[AH + 1];
+#pragma unroll
+            for (int s = 0; s < AH; ++s) frag(s, fa[s], fb[s]);
+#pragma unroll
+            for (int s = 0; s < 36; ++s) {
+                if (s + AH < 36) frag(s + AH, fa[(s + AH) % (AH + 1)], fb[(s + AH) % (AH + 1)]);
+                const int c = s % (AH + 1);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[c], fb[c], acc, 0, 0, 0);
             }
         };
         conv_part(0);
@@ -1003,18 +1015,25 @@ __global__ __launch_bounds__(512) void k_dec_conv4s(DecConvArgs a) {
     };
     f16x acc[2];
     auto conv_part = [&]() {
-#pragma unroll 4
-        for (int s = 0; s < 36; ++s) {
+        // fragments read PVC_L1_AHEAD k-steps ahead of their MFMAs (k_conv64)
+        auto frag = [&](int s, h8 &bf, h8 &a0, h8 &a1) {
             const int o = 2 * s + h;
             const int tap = o >> 3, q = o & 7;
             const int ky = tap / 3, kx = tap - 3 * ky;
-            const int hp = (wid + ky) * kHC + n + kx;
-            const h8 bf = *(const h8 *)(halo + halo_granule(hp, q) * 16);
+            bf = *(const h8 *)(halo + halo_granule((wid + ky) * kHC + n + kx, q) * 16);
+            a0 = *(const h8 *)(wl + ((o * 2 + 0) * 32 + n) * 16);
+            a1 = *(const h8 *)(wl + ((o * 2 + 1) * 32 + n) * 16);
+        };
+        constexpr int AH = PVC_L1_AHEAD;
+        h8 fb[AH + 1], f0[AH + 1], f1[AH + 1];
 #pragma unroll
-            for (int m = 0; m < 2; ++m) {
-                const h8 af = *(const h8 *)(wl + ((o * 2 + m) * 32 + n) * 16);
-                acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[m], 0, 0, 0);
-            }
+        for (int s = 0; s < AH; ++s) frag(s, fb[s], f0[s], f1[s]);
+#pragma unroll
+        for (int s = 0; s < 36; ++s) {
+            if (s + AH < 36) frag(s + AH, fb[(s + AH) % (AH + 1)], f0[(s + AH) % (AH + 1)], f1[(s + AH) % (AH + 1)]);
+            const int c = s % (AH + 1);
+            acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f0[c], fb[c], acc[0], 0, 0, 0);
+            acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f1[c], fb[c], acc[1], 0, 0, 0);
         }
     };
     int tile = (int)blockIdx.x;
@@ -1132,30 +1151,43 @@ __global__ __launch_bounds__(512) void k_conv64(L1Args a) {
         }
         __syncthreads();
         if (tile + (int)gridDim.x < a.ntiles) fetch(tile + (int)gridDim.x);
+        // this lane's residual, loaded now so its latency hides behind the convolution
+        const int oy = y0 + wid, ox = x0 + n;
+        const bool pix_ok = oy < a.H && ox < a.W;
+        const int64_t po = (((int64_t)b * a.H + (pix_ok ? oy : 0)) * a.W + (pix_ok ? ox : 0)) * 64;
+        h4 r[2][4];
+        if (a.res) {
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) r[m][g] = *(const h4 *)(a.res + po + 32 * m + 8 * g + 4 * h);
+        }
         f16x acc[2] = {};
-#pragma unroll 4
-        for (int s = 0; s < 36; ++s) {
+        // k-step s's fragments: the halo pixel's 8 channels (B) and the two
+        // 32-cout weight rows (A).  Read PVC_L1_AHEAD steps ahead of their
+        // MFMAs: at 2 waves per SIMD a read issued right before its MFMA
+        // leaves the LDS latency exposed on every step.
+        auto frag = [&](int s, h8 &bf, h8 &a0, h8 &a1) {
             const int o = 2 * s + h;          // octet of this lane half: tap o / 8, channels 8 (o % 8)
             const int tap = o >> 3, q = o & 7;
             const int ky = tap / 3, kx = tap - 3 * ky;
-            const h8 bf = *(const h8 *)(halo + halo_granule((wid + ky) * kHC + n + kx, q) * 16);
+            bf = *(const h8 *)(halo + halo_granule((wid + ky) * kHC + n + kx, q) * 16);
+            a0 = *(const h8 *)(wl + ((o * 2 + 0) * 32 + n) * 16);
+            a1 = *(const h8 *)(wl + ((o * 2 + 1) * 32 + n) * 16);
+        };
+        constexpr int AH = PVC_L1_AHEAD;
+        h8 fb[AH + 1], f0[AH + 1], f1[AH + 1];
 #pragma unroll
-            for (int m = 0; m < 2; ++m) {
-                const h8 af = *(const h8 *)(wl + ((o * 2 + m) * 32 + n) * 16);
-                acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[m], 0, 0, 0);
-            }
+        for (int s = 0; s < AH; ++s) frag(s, fb[s], f0[s], f1[s]);
+#pragma unroll
+        for (int s = 0; s < 36; ++s) {
+            if (s + AH < 36) frag(s + AH, fb[(s + AH) % (AH + 1)], f0[(s + AH) % (AH + 1)], f1[(s + AH) % (AH + 1)]);
+            const int c = s % (AH + 1);
+            acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f0[c], fb[c], acc[0], 0, 0, 0);
+            acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f1[c], fb[c], acc[1], 0, 0, 0);
         }
         // ---- epilogue: acc[m] rows (i & 3) + 8 (i >> 2) + 4 h = couts 32 m + .., column n = pixel ----
-        const int oy = y0 + wid, ox = x0 + n;
-        if (oy < a.H && ox < a.W) {
-            const int64_t po = (((int64_t)b * a.H + oy) * a.W + ox) * 64;
-            h4 r[2][4];
-            if (a.res) {
-#pragma unroll
-                for (int m = 0; m < 2; ++m)
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) r[m][g] = *(const h4 *)(a.res + po + 32 * m + 8 * g + 4 * h);
-            }
+        if (pix_ok) {
 #pragma unroll
             for (int m = 0; m < 2; ++m)
 #pragma unroll

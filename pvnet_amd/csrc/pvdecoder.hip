@@ -113,10 +113,11 @@ __global__ __launch_bounds__(256) void k_epilogue(const T *__restrict__ x, const
     constexpr int V = 16 / sizeof(T);
     typedef typename Vec<T, V>::type vT;
     const int c1v = C1 / V, cv = (C1 + C2) / V, Co = C1 + C2;
-    const int64_t n = P * cv;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        const int64_t p = i / cv;
-        const int k = (int)(i - p * cv);
+    const uint32_t n = (uint32_t)(P * cv);        // < 2^31 (host): 32-bit division, not 64-bit
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        const uint32_t p32 = i / (uint32_t)cv;
+        const int k = (int)(i - p32 * (uint32_t)cv);
+        const int64_t p = p32;
         vT v;
         if (k < c1v) {
             v = *(const vT *)(x + p * C1 + V * k);
@@ -155,6 +156,7 @@ int epilogue(const void *x, const void *bias, const void *res, const void *rbias
     if (c2 > 0 && out == x) return PV_EINVAL;     // in place only without the skip channels
     if (P == 0) return PV_OK;
     const int64_t n = P * ((c1 + c2) / V);
+    if (n >= (1ll << 31)) return PV_EINVAL;       // the kernel's 32-bit element index
     const int64_t blocks = (n + 255) / 256;
     k_epilogue<T><<<(unsigned)(blocks < 256 * 64 ? blocks : 256 * 64), 256, 0, (hipStream_t)stream>>>(
         (const T *)x, (const T *)bias, (const T *)res, (const T *)rbias, (const T *)skip, (T *)out, P, c1, c2, act,
@@ -179,14 +181,15 @@ __global__ __launch_bounds__(256) void k_relu_pool(const T *__restrict__ x, cons
                                                    int C, int Ho, int Wo) {
     constexpr int V = 16 / sizeof(T);
     typedef typename Vec<T, V>::type vT;
-    const int cv = C / V;
-    const int64_t total = (int64_t)N * Ho * Wo * cv;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-        const int k = (int)(i % cv);
-        const int64_t p = i / cv;
-        const int px = (int)(p % Wo);
-        const int64_t q = p / Wo;
-        const int py = (int)(q % Ho), b = (int)(q / Ho);
+    // 32-bit index arithmetic (the host keeps total < 2^31): a 64-bit
+    // division is a long software sequence on the GPU, three of them per
+    // element made this pass index-bound
+    const uint32_t cv = (uint32_t)(C / V);
+    const uint32_t total = (uint32_t)N * Ho * Wo * cv;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+        const uint32_t p = i / cv, k = i - p * cv;
+        const uint32_t q = p / (uint32_t)Wo, px = p - q * (uint32_t)Wo;
+        const uint32_t b = q / (uint32_t)Ho, py = q - b * (uint32_t)Ho;
         vT bv = {};
         if (bias) bv = *(const vT *)(bias + V * k);
         vT m;
@@ -194,11 +197,11 @@ __global__ __launch_bounds__(256) void k_relu_pool(const T *__restrict__ x, cons
         for (int e = 0; e < V; ++e) m[e] = (T)(-INFINITY);
 #pragma unroll
         for (int dy = -1; dy <= 1; ++dy) {
-            const int iy = 2 * py + dy;
+            const int iy = 2 * (int)py + dy;
             if (iy < 0 || iy >= H) continue;
 #pragma unroll
             for (int dx = -1; dx <= 1; ++dx) {
-                const int ix = 2 * px + dx;
+                const int ix = 2 * (int)px + dx;
                 if (ix < 0 || ix >= W) continue;
                 const int64_t off = (((int64_t)b * H + iy) * W + ix) * C + V * k;
                 vT v = *(const vT *)(x + off);
@@ -213,7 +216,7 @@ __global__ __launch_bounds__(256) void k_relu_pool(const T *__restrict__ x, cons
                 if (bias && dy >= 0 && dx >= 0) *(vT *)(x2s + off) = v;
             }
         }
-        *(vT *)(pool + p * C + V * k) = m;
+        *(vT *)(pool + (int64_t)p * C + V * k) = m;
     }
 }
 
@@ -228,6 +231,7 @@ int relu_pool(const void *x, const void *bias, void *x2s, void *pool, int32_t n,
     if (n == 0) return PV_OK;
     const int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;     // kernel 3, stride 2, pad 1
     const int64_t total = (int64_t)n * ho * wo * (c / V);
+    if (total >= (1ll << 31)) return PV_EINVAL;   // the kernel's 32-bit element index
     const int64_t blocks = (total + 255) / 256;
     k_relu_pool<T><<<(unsigned)(blocks < 256 * 64 ? blocks : 256 * 64), 256, 0, (hipStream_t)stream>>>(
         (const T *)x, (const T *)bias, (T *)x2s, (T *)pool, n, h, w, c, ho, wo);
