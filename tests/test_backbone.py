@@ -814,3 +814,23 @@ def test_conv64_matches_torch(case, device):
     print(f"conv64 {case}: max dev {float(d.max()):.3e}, mean {float(d.mean()):.2e} (scale {sc:.2f})")
     assert float(d.max()) <= 2 ** -8 * sc
     assert float(d.mean()) <= 2 ** -13 * sc
+
+def test_conv3x3_ex_eligibility():
+    """Which convolutions PVNetInference routes to pv_conv3x3_ex_f16 (CPU):
+    3x3, stride 1 or 2, padding = dilation, Cin % 64, Cout % 128; and which
+    downsamples it sums into conv2 (a 1x1 conv with bias, the folded BN left
+    as an Identity)."""
+    from torch import nn
+    from pvnet_amd.network import PVNet, conv3x3_eligible, downsample_eligible, fold_batchnorm
+    assert conv3x3_eligible(nn.Conv2d(64, 128, 3, 2, 1))
+    assert conv3x3_eligible(nn.Conv2d(256, 512, 3, 1, 4, 4))
+    assert not conv3x3_eligible(nn.Conv2d(64, 128, 3, 3, 1))
+    assert not conv3x3_eligible(nn.Conv2d(64, 96, 3, 1, 1))
+    assert not conv3x3_eligible(nn.Conv2d(32, 128, 3, 1, 1))
+    assert not conv3x3_eligible(nn.Conv2d(64, 128, 3, 1, 2, 1))
+    f = fold_batchnorm(PVNet(18, 2).eval())
+    r = f.resnet18_8s
+    dss = [blk.downsample for layer in (r.layer2, r.layer3, r.layer4) for blk in layer if blk.downsample is not None]
+    assert len(dss) == 3 and all(downsample_eligible(d) for d in dss)
+    assert not downsample_eligible(None)
+    assert not downsample_eligible(nn.Sequential(nn.Conv2d(64, 128, 1, 2, bias=False)))
