@@ -534,6 +534,59 @@ def measure_pose(dev, b=32, steps=5):
                 note="synthetic box-keypoint fields (0.05 rad noise, 20% outliers); error vs the generating pose")
 
 
+def measure_e2e_config4(dev, batch=32, iters=10):
+    """configs[4] end to end on one GPU: the YCB-Video network PVnet(42, 2)
+    (21 keypoints; MR:7-79 with ver_dim 42) in the fp16 channels-last
+    inference form, then ransac_voting_layer_v3 from its outputs,
+    estimate_voting_distribution_with_mean (16 rounds x 256 hypotheses) on
+    argmax(seg) and the strided vertex view, and the uncertainty PnP of all
+    21 keypoints -- one hipGraph per batch of 32 480x640 frames.
+    Random-init weights (none ship with the reference): timing only."""
+    from pvnet_amd import extend_utils as eu
+    from pvnet_amd import ransac_voting_gpu as rvg
+    from pvnet_amd.network import PVNet, PVNetInference
+    torch.manual_seed(0)
+    H, W, KP = 480, 640, 21
+    net = PVNetInference(PVNet(2 * KP, 2).eval()).to(dev).half().to(memory_format=torch.channels_last)
+    x = torch.randn(batch, 3, H, W, device=dev).half().contiguous(memory_format=torch.channels_last)
+    rng = np.random.default_rng(5)
+    p3 = torch.from_numpy(rng.uniform(-0.06, 0.06, size=(KP, 3))).to(dev)
+    K = torch.tensor([[1066.778, 0.0, 312.9869], [0.0, 1067.487, 241.3109], [0.0, 0.0, 1.0]],
+                     dtype=torch.float64, device=dev)              # the YCB-Video camera
+    w1, w2 = rvg.VotingWorkspace(), rvg.VotingWorkspace()
+
+    def once():
+        with torch.no_grad():
+            seg, ver = net(x)
+            mean = rvg.ransac_voting_layer_v3_from_network(seg, ver, 512, _workspace=w1, _seed=13)
+            mask = seg.argmax(1)
+            vertex = ver.permute(0, 2, 3, 1).view(batch, H, W, KP, 2)
+            mean, cov = rvg.estimate_voting_distribution_with_mean(mask, vertex, mean, _workspace=w2, _seed=14)
+            return eu.uncertainty_pnp_batch(mean, cov, p3, K, mode="cov")
+
+    s = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            once()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            Rt = once()
+    g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        g.replay()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / iters
+    return dict(images_per_s=round(batch / dt, 1), ms_per_batch=round(dt * 1e3, 4), batch=batch, keypoints=KP,
+                backbone="PVnet(42, 2) fp16 channels-last inference form", poses_finite=int(torch.isfinite(Rt).all(-1).all(-1).sum()),
+                stages="backbone + v3 (hn 512) + EVD with mean (16 x 256) + uncertainty PnP (21 points), one hipGraph",
+                note="random-init weights (none ship with the reference): timing only; parity of each stage: "
+                     "tests/test_backbone.py (PVnet(42, 2) vs G4), tests/test_gpu_pnp.py, tests/test_gpu_parity.py")
+
+
 FP16_MFMA_DENSE_TFLOPS = 2500.0      # MI355X dense fp16/bf16 matrix peak (no sparsity)
 FP32_MATRIX_TFLOPS = 157.3           # f32 MFMA = the vector peak (MI355X_MICROARCH.md)
 BACKBONE_GFLOP = 144.9               # ResNet-18 OS8 seg+vertex forward at 480x640 (SURVEY 8(a) A8)
@@ -798,7 +851,8 @@ def report(args, ws, res, final_err, dev):
                         ("e2e_config2_fp16_batch32", lambda: measure_e2e(dev, half=True, batch=32)),
                         ("voting_config2_batch32", lambda: measure_batch(dev)),
                         ("pnp_config5", lambda: measure_pnp(dev)),
-                        ("pose_config5_batch32", lambda: measure_pose(dev))):
+                        ("pose_config5_batch32", lambda: measure_pose(dev)),
+                        ("e2e_config4_fp16_batch32", lambda: measure_e2e_config4(dev))):
             try:
                 line[key] = fn()
             except Exception as e:
