@@ -400,6 +400,13 @@ def conv3x3(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, dil: int, act:
 
 
 _CONV_WS: dict = {}
+
+
+def clear_conv_workspaces() -> None:
+    """Drop every split-K scratch buffer (no captured graph that used one may
+    be replayed afterwards)."""
+    _CONV_WS.clear()
+
 CONV_SPLIT = True          # the split-K last round (A/B hook for tools/backbone_ab2.py; no environment switch)
 
 
@@ -408,7 +415,9 @@ def _conv_workspace(x: torch.Tensor, pixels: int, cout: int, ksteps: int):
     tiles): one buffer per (device, stream), since calls on one stream run in
     order; grown to the largest need and kept, so a captured graph keeps
     using the buffer it captured (a buffer first made during a capture comes
-    from the graph's pool).  (pointer, bytes) or (None, 0)."""
+    from the graph's pool).  A process that keeps creating streams should
+    call :func:`clear_conv_workspaces` once their graphs are gone.
+    (pointer, bytes) or (None, 0)."""
     from pvnet_amd import _lib
     need = int(_lib.load().pv_conv3x3_workspace_bytes(pixels, cout, ksteps))
     if need <= 0 or not CONV_SPLIT:
