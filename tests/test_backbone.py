@@ -486,6 +486,23 @@ def test_relu_maxpool_matches_torch(dtype, hw, device):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
+@pytest.mark.parametrize("hw", [(240, 320), (37, 51), (10, 7), (3, 2)])
+def test_maxpool_matches_torch(dtype, hw, device):
+    """The pool-only form of pv_relu_maxpool (the stem kernel's maxpool,
+    RN:204) is bit-equal to ATen's max_pool2d(3, 2, 1), odd and tiny maps
+    included."""
+    from pvnet_amd.network import maxpool
+    g = torch.Generator().manual_seed(hw[0] * 100 + hw[1])
+    cl = torch.channels_last
+    x = torch.randn(2, 64, *hw, generator=g).to(device, dtype).contiguous(memory_format=cl)
+    got = maxpool(x)
+    ref = torch.nn.functional.max_pool2d(x, 3, 2, 1)
+    assert got.shape == ref.shape and got.is_contiguous(memory_format=cl)
+    assert torch.equal(got, ref)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("case", ["relu_128_256_d2", "res_256_256_d2", "resb_256_512_d4", "relu_512_512_d4",
                                   "fc_512_256_d1_ragged", "leaky_64_256_d1", "resb_128_128_d1",
                                   "leaky_384_128_d1_ragged", "resb_256_512_d4_big", "relu_128_128_d1_big"])
