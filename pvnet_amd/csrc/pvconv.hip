@@ -38,6 +38,9 @@
 
 #include "../../include/pvvote.h"
 
+#ifndef PVC_PT_MAJOR
+#define PVC_PT_MAJOR 1      // k_conv3x3 tile order within an XCD's range: 1 pixel tile major (5.41-5.45 -> 5.29 ms backbone), 0 cout tile major
+#endif
 #ifndef PVC_L1_AHEAD
 #define PVC_L1_AHEAD 2      // halo kernels (k_conv64, k_dec_conv2s / 4s): fragment reads this many k-steps ahead of their MFMAs
 #endif
@@ -461,7 +464,7 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STAGE];
     const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
     // XCD-aware tile order: blocks i, i + 8, ... share an XCD; give each XCD a
-    // contiguous range of tiles, cout tile major
+    // contiguous range of tiles, pixel tile major (PVC_PT_MAJOR)
     // The last partial round of tiles (ntiles mod CUs) is cut into nsplit K
     // parts run by nsplit blocks each (dispatched last), so that round ends
     // nsplit x sooner; the part that arrives last sums the others' f32
@@ -476,7 +479,11 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
         part = j - tail * a.nsplit;
         bid = a.nfull + tail;
     }
+#if PVC_PT_MAJOR
+    const int ct = bid % a.nct, pt = bid / a.nct;     // a pixel tile's cout tiles adjacent (same XCD, same time)
+#else
     const int ct = bid / a.ntp, pt = bid % a.ntp;
+#endif
     const int n0 = ct * CT;
     const int64_t p0 = (int64_t)pt * kPT;
     const __amdgpu_buffer_rsrc_t wr =
