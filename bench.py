@@ -14,6 +14,10 @@ the timed region.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--per-step M]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
+With --gpus N > 1 and no torchrun environment (WORLD_SIZE unset) the process
+starts the N ranks itself (launch_ranks: one child per GPU carrying RANK /
+LOCAL_RANK / WORLD_SIZE / MASTER_*, before this process makes any GPU call).
+
 Prints ONE JSON line on rank 0 (contract in the task statement).
 """
 from __future__ import annotations
@@ -80,14 +84,78 @@ def parse():
     ap.add_argument("--skip-e2e", action="store_true")
     ap.add_argument("--skip-u1", action="store_true")
     ap.add_argument("--skip-config3", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="the multi-rank plumbing without a GPU (CPU tests): gloo ranks, each image's result is its "
+                         "field's generating keypoints (no voting), then the timed region's barriers, the gather, "
+                         "the max over ranks and the stream-order check of a real run; the line says dry_run")
     return ap.parse_args()
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` (N > 1) outside torchrun: start the N ranks as child
+    processes (the script again, RANK = LOCAL_RANK = r, WORLD_SIZE = N,
+    MASTER_ADDR 127.0.0.1 and a free port) and wait for them.  This process
+    makes no GPU call: it only counts the devices (torch.cuda.device_count()
+    does not initialise HIP) and fails if fewer than N are visible.  Rank 0
+    prints the JSON line.  If a rank fails, the others (this process's own
+    children, by PID) are terminated.  Returns the exit code."""
+    import signal
+    import socket
+    import subprocess
+    n = args.gpus
+    if not args.dry_run:
+        have = torch.cuda.device_count()
+        if have < n:
+            log(f"bench.py --gpus {n}: only {have} GPU(s) visible")
+            return 2
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
+               LOCAL_WORLD_SIZE=str(n))
+    cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    # rank 0's stdout is this process's (the JSON line); the others' goes to stderr
+    procs = [subprocess.Popen(cmd, env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
+                              stdout=None if r == 0 else sys.stderr) for r in range(n)]
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+    signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
+    rc, live = 0, list(procs)
+    try:
+        while live:
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    log(f"rank {procs.index(p)} exited with {c}: stopping the other ranks")
+                    stop()
+            time.sleep(0.1)
+    except KeyboardInterrupt:
+        stop()
+        raise
+    return rc
 
 
 def setup_dist(args):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws != args.gpus:
+        raise SystemExit(f"WORLD_SIZE {ws} != --gpus {args.gpus}")
+    if args.dry_run:
+        if ws > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo")
+        return ws, rank, torch.device("cpu")
     if ws > 1:
+        if torch.cuda.device_count() <= local:
+            raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but {torch.cuda.device_count()} GPU(s) visible")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -198,12 +266,67 @@ def run_stream(args, ws, rank, dev, segs, vers, steps, seed_base):
         elapsed = float(t.item())
         mine_t = torch.tensor(mine, device=dev)
         assert torch.equal(allkp[mine_t], local), "gathered stream order differs from the shard"
-    return elapsed, local, works, s
+    return elapsed, local, works, s, allkp
+
+
+def stream_order_error(allkp, ws, nfields):
+    """Max |keypoint - generating keypoint| over the gathered stream: image i
+    (voted by rank i % ws) against S(field_seed(i)), so a result gathered into
+    the wrong slot shows as an error of tens of pixels."""
+    from pvnet_amd import synth
+    seeds = [field_seed(i, ws, nfields) for i in range(nfields * ws)]
+    ref = np.stack([synth.field_keypoints(sd) for sd in seeds]).astype(np.float32)
+    got = allkp.cpu().numpy()
+    return float(np.abs(got - ref[np.arange(got.shape[0]) % (nfields * ws)]).max())
+
+
+def dry_run(args, ws, rank):
+    """--dry-run (CPU, gloo): the launcher, the shard, the timed region's
+    barriers, the gather, the max over ranks and the stream-order check, with
+    each image's result = its field's generating keypoints (nothing is voted);
+    rank 0 prints a line of the real run's form marked dry_run."""
+    from pvnet_amd import distributed as D
+    from pvnet_amd import synth
+    K, M, NF = args.steps, args.per_step, max(1, args.fields)
+    n_images = ws * K * M
+    mine = D.shard(n_images, rank, ws)
+    if ws > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    local = torch.from_numpy(np.stack([synth.field_keypoints(field_seed(i, ws, NF)) for i in mine]).astype(np.float32))
+    allkp = D.gather_results(local, n_images, rank, ws)
+    if ws > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    err = stream_order_error(allkp, ws, NF)
+    if rank == 0:
+        line = {"metric": "images/sec (480x640, 9 kp) vote->keypoint", "value": round(n_images / elapsed, 2),
+                "unit": "images/sec", "n_gpus": ws, "steps": K, "warmup": args.warmup,
+                "ms_per_step": round(elapsed / K * 1e3, 5), "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": None, "dtype": "f32", "data": "none (dry run)", "dry_run": True,
+                "config": {"workload": "dry run: launcher + shard + gather only, no voting", "global_batch": M * ws,
+                           "per_gpu_batch_per_step": M, "stream_images": n_images},
+                "stream_order_max_err_px": err, "stream_order_ok": err == 0.0}
+        assert line["n_gpus"] == args.gpus
+        if not args.skip_cpu:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if ws > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        raise SystemExit(launch_ranks(args))
     ws, rank, dev = setup_dist(args)
+    if args.dry_run:
+        return dry_run(args, ws, rank)
     from pvnet_amd import ransac_voting_gpu as rvg
 
     M, K, NF = args.per_step, args.steps, max(1, args.fields)
@@ -211,7 +334,11 @@ def main():
     segs, vers, kps, tn = make_fields(rank, ws, NF, dev)
     # local image j (stream image rank + ws * j) votes field j % NF: field_seed == 1234 + rank + ws * (j % NF)
     assert all(field_seed(rank + ws * j, ws, NF) == 1234 + rank + ws * (j % NF) for j in range(4 * NF))
-    elapsed, local, works, s = run_stream(args, ws, rank, dev, segs, vers, K, 0)
+    elapsed, local, works, s, allkp = run_stream(args, ws, rank, dev, segs, vers, K, 0)
+    # every gathered image against its field's generating keypoints: a result
+    # in the wrong stream slot would be tens of pixels off
+    order_err = stream_order_error(allkp, ws, NF)
+    del allkp
     out_step = torch.zeros((M, VN, 2), dtype=torch.float32, device=dev)
 
     # sanity on the timed outputs: every local image against its field's
@@ -250,7 +377,7 @@ def main():
     torch.cuda.synchronize()
     latency_ms = (time.perf_counter() - t1) / NLAT * 1e3
     res = dict(elapsed=elapsed, vote_ms=vote_ms, compact_ms=compact_ms, tn=tn, latency_ms=latency_ms,
-               n_images=n_images, config3=c3)
+               n_images=n_images, config3=c3, order_err=order_err)
     if rank == 0:
         report(args, ws, res, err, dev)
     if ws > 1:
@@ -265,7 +392,7 @@ def stream_config3(args, ws, rank, dev, steps=8):
     once; images/s over all ranks (max-over-ranks wall time)."""
     NF = max(8, args.fields)
     segs, vers, kps, tns, kinds = make_stream_fields(rank, ws, NF, dev)
-    elapsed, local, _, _ = run_stream(args, ws, rank, dev, segs, vers, steps, 50_000)
+    elapsed, local, _, _, _ = run_stream(args, ws, rank, dev, segs, vers, steps, 50_000)
     n = ws * steps * args.per_step
     lk = local.cpu().numpy()
     j = np.arange(lk.shape[0]) % NF
@@ -385,6 +512,63 @@ def measure_u1(dev, hn=512, reps=100):
                 traffic=pmc_traffic("k_vote_bytes"), ms=ms,
                 achieved_gbs=nbytes / (ms * 1e-3) / 1e9, peak_gbs=HBM_PEAK_GBS,
                 frac=nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, hn=hn, tn=tn)
+
+
+def measure_u4(dev, reps=20):
+    """U4: estimate_voting_distribution_with_mean (RV:333-406)
+    on S(1234) -- 16 rounds x 256 hypotheses = one vote/count launch over 4096
+    hypotheses per keypoint, then the covariance reduction (k_evd_with_mean).
+    hipEvents the library records on the launching stream around the vote
+    kernel (pv_estimate_voting_distribution_with_mean_diag), plus one after
+    the call for the reduction; eager calls, medians over `reps`."""
+    import ctypes
+    from pvnet_amd import _lib
+    from pvnet_amd import ransac_voting_gpu as rvg
+    from pvnet_amd import synth
+    f = synth.synthetic_field(1234)
+    mask = torch.from_numpy(np.argmax(f["seg"], 1)).to(dev)
+    vertex = torch.from_numpy(np.ascontiguousarray(f["vertex"].transpose(0, 2, 3, 1).reshape(1, H, W, VN, 2))).to(dev)
+    mean = torch.from_numpy(f["keypoints"].astype(np.float32)[None]).to(dev)
+    work = rvg.VotingWorkspace()
+    L = _lib.load()
+    s = torch.cuda.Stream(device=dev)
+    ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(5)) for _ in range(reps + 3)]
+    cov = torch.empty((1, VN, 2, 2), dtype=torch.float32, device=dev)
+    with torch.cuda.stream(s):
+        for e5 in ev:
+            for e in e5:
+                e.record(s)
+        torch.cuda.synchronize()
+        for k, (c0, c1, v0, v1, e1) in enumerate(ev):
+            d, prm, ws, nbytes, keep = rvg._evd_common(mask, vertex, 256, 4096, 0.99, 20, 30000, 128, None, None,
+                                                        1000 + k, work)
+            dd = _lib.V3Diag(ev_vote_begin=v0.cuda_event, ev_vote_end=v1.cuda_event, ev_compact_end=c1.cuda_event)
+            c0.record(s)
+            _lib.check(L.pv_estimate_voting_distribution_with_mean_diag(
+                ctypes.byref(d), ctypes.byref(prm), mean.data_ptr(), cov.data_ptr(), ws.data_ptr(), nbytes,
+                ctypes.byref(dd), s.cuda_stream), "pv_estimate_voting_distribution_with_mean_diag")
+            e1.record(s)
+    torch.cuda.synchronize()
+    ev = ev[3:]                                   # the first calls size the workspace and warm up
+    vote = np.array([v0.elapsed_time(v1) for _, _, v0, v1, _ in ev])
+    red = np.array([v1.elapsed_time(e1) for _, _, _, v1, e1 in ev])
+    call = np.array([c0.elapsed_time(e1) for c0, _, _, _, e1 in ev])
+    tn = int(f["tn"])
+    flops = 12.0 * 4096 * VN * tn                # 16 x U2 at hn 256: 12 FLOP per (hypothesis, keypoint, pixel)
+    vm = float(np.median(vote))
+    achieved = flops / (vm * 1e-3) / 1e12
+    c = cov.cpu().numpy()
+    return dict(bound="valu", kernel="k_vote_mfma at n_hyp 4096 (U4's 16 x 256 hypotheses) + k_evd_with_mean",
+                achieved=round(achieved, 2), peak=FP32_VECTOR_PEAK_TFLOPS, unit="TFLOP/s",
+                frac=round(achieved / FP32_VECTOR_PEAK_TFLOPS, 4), avg_kernel_ms=round(vm, 5),
+                flop_per_launch=flops, reduce_ms=round(float(np.median(red)), 5),
+                call_ms=round(float(np.median(call)), 5), tn=tn, hyp=4096, samples=len(ev),
+                traffic=pmc_traffic("k_vote_mfma_evd"), cov_finite=bool(np.isfinite(c).all()),
+                note="estimate_voting_distribution_with_mean on S(1234) (tn 29,861, 9 kp): FLOP = 16 x 12 x 256 x vn "
+                     "x tn (SURVEY 8(d) U4) / the median vote-kernel time between hipEvents the library records "
+                     "around it on its stream (eager calls); reduce_ms = the covariance reduction "
+                     "(k_evd_with_mean) to the call's end, call_ms = the whole call (compaction + hypotheses + "
+                     "vote + reduction); rocprof durations of the same command: %s" % STATS_FILE)
 
 
 def config2_fields(b=32):
@@ -817,6 +1001,8 @@ def report(args, ws, res, final_err, dev):
         "roofline_vote_count": vc,
         "roofline_compaction": rc,
         "max_kp_err_px": round(final_err, 5),
+        "stream_order_max_err_px": round(res["order_err"], 5),
+        "stream_order_ok": res["order_err"] <= 5.0,
         "latency_ms_per_image": round(res["latency_ms"], 5),
         "library": library_config(),
     }
@@ -846,6 +1032,10 @@ def report(args, ws, res, final_err, dev):
                                          "traffic = 2*FETCH_SIZE + WRITE_SIZE per launch (%s)" % (STATS_FILE, PMC_FILE))
         except Exception as e:  # reported, never hides the main number
             line["roofline"] = {"error": repr(e)}
+    try:
+        line["roofline_evd"] = measure_u4(dev)
+    except Exception as e:  # reported, never hides the main number
+        line["roofline_evd"] = {"error": repr(e)}
     if not args.skip_e2e:
         for key, fn in (("e2e_config1", lambda: measure_e2e(dev)),
                         ("e2e_config2_fp16_batch32", lambda: measure_e2e(dev, half=True, batch=32)),
@@ -857,8 +1047,9 @@ def report(args, ws, res, final_err, dev):
                 line[key] = fn()
             except Exception as e:
                 line[key] = {"error": repr(e)}
-    if ws == 1 and not args.skip_cpu:
+    if not args.skip_cpu:       # rank 0, at every N (the other ranks wait at the final barrier)
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    assert line["n_gpus"] == args.gpus, (line["n_gpus"], args.gpus)
     print(json.dumps(line), flush=True)
 
 

@@ -150,6 +150,14 @@ int pv_estimate_voting_distribution_with_mean(const pv_image_desc *img, const pv
                                               const float *mean, float *cov, void *workspace,
                                               size_t workspace_bytes, pv_stream_t stream);
 
+/* The same with the diag's timing events (ev_compact_end, ev_vote_begin / ev_vote_end around the
+ * vote/count kernel at n_hyp = rounds x round_hyp_num); its other fields are ignored.  Diagnostics
+ * only (bench.py's U4 line); not part of the reference's interface. */
+int pv_estimate_voting_distribution_with_mean_diag(const pv_image_desc *img, const pv_vote_params *prm,
+                                                   const float *mean, float *cov, void *workspace,
+                                                   size_t workspace_bytes, const pv_v3_diag *diag,
+                                                   pv_stream_t stream);
+
 /* estimate_voting_distribution (RV:263-331): mean out [b,vn,2], cov out [b,vn,2,2].
  * topk ties at the k-th ratio are taken lowest-hypothesis-index first. */
 int pv_estimate_voting_distribution(const pv_image_desc *img, const pv_vote_params *prm, float *mean,

@@ -71,6 +71,8 @@ SIGNATURES = [
     ("pv_ransac_motion_voting", ctypes.c_int, [ctypes.POINTER(ImageDesc), c_vp, c_vp]),
     ("pv_estimate_voting_distribution_with_mean", ctypes.c_int,
      [ctypes.POINTER(ImageDesc), ctypes.POINTER(VoteParams), c_vp, c_vp, c_vp, c_size, c_vp]),
+    ("pv_estimate_voting_distribution_with_mean_diag", ctypes.c_int,
+     [ctypes.POINTER(ImageDesc), ctypes.POINTER(VoteParams), c_vp, c_vp, c_vp, c_size, ctypes.POINTER(V3Diag), c_vp]),
     ("pv_estimate_voting_distribution", ctypes.c_int,
      [ctypes.POINTER(ImageDesc), ctypes.POINTER(VoteParams), c_vp, c_vp, c_vp, c_size, c_vp]),
     ("pv_uncertainty_pnp", ctypes.c_int, [ctypes.POINTER(PnpBatch), c_vp, ctypes.POINTER(PnpDiag), c_vp]),

@@ -449,6 +449,12 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_ba
 #ifndef PVC_NW
 #define PVC_NW 16
 #endif
+#ifndef PVC_CB_MAJOR
+#define PVC_CB_MAJOR 1
+#endif
+#ifndef PVC_ISSUE_MID
+#define PVC_ISSUE_MID 2          // 0 before the step's MFMAs, 1 after its first half, 2 = 1 for 256-cout tiles only
+#endif
 constexpr int kNW = PVC_NW;                   // waves per block: 16 (4 cout x 4 pixel groups; 8 = 2 x 4 measured 5-8 % slower)
 
 template <int CT>
@@ -499,8 +505,13 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
     const int cbk = a.cblocks;               // channel blocks per tap (both inputs' for a cat)
     const int ksteps = a.ksteps;
     // this lane's NW weight and NI pixel granules per stage: granule g = (N wid + i) 64 + lane
-    int woff[NW], py[NI], px[NI], iy[NI], sg16[NI];
-    bool pin[NI];
+    int woff[NW];
+    // per pixel granule: its output pixel's input position (stride applied;
+    // far out of range for rows past the map) and its byte offset in x (and in
+    // x2: the same pixel of the cat's second map, or the 1x1 input's pixel),
+    // segment included -- a step adds one wave-uniform tap / channel delta
+    int pyb[NI], pxb[NI];
+    uint32_t pb1[NI], pb2[NI];
 #pragma unroll
     for (int i = 0; i < NW; ++i) {
         const int g = (NW * wid + i) * 64 + lane, row = g / GPR, pseg = g % GPR;
@@ -512,42 +523,60 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
         const int g = (NI * wid + i) * 64 + lane, row = g / GPR, pseg = g % GPR;
         const int seg = conv_granule(row, pseg) - row * GPR;
         const int64_t p = p0 + row;
-        pin[i] = p < a.M;
-        const int64_t pc = pin[i] ? p : 0;
+        const bool pin = p < a.M;
+        const int64_t pc = pin ? p : 0;
         const int img = (int)(pc / ((int64_t)a.H * a.W)), rem = (int)(pc - (int64_t)img * a.H * a.W);
-        py[i] = rem / a.W;
-        px[i] = rem - py[i] * a.W;
-        iy[i] = img;
-        sg16[i] = seg * 16;
+        const int py = rem / a.W, px = rem - py * a.W;
+        pyb[i] = pin ? py * a.stride : -(1 << 28);
+        pxb[i] = px * a.stride;
+        const int pix = (img * a.Hin + py * a.stride) * a.Win + px * a.stride;
+        pb1[i] = (uint32_t)(pix * a.Cin * 2 + seg * 16);
+        if (a.mode2 == PV_CONV_X2_1X1)
+            pb2[i] = pin ? (uint32_t)(((img * a.H2 + py * a.s2) * a.W2 + px * a.s2) * a.Cin2 * 2 + seg * 16)
+                         : 0x80000000u;
+        else
+            pb2[i] = (uint32_t)(pix * a.Cin2 * 2 + seg * 16);
     }
+#if PVC_CB_MAJOR
+    // K order: step s of the 3x3 part is (channel block s / 9, tap s % 9): a
+    // tile's nine taps read the same channel block of its (dilated) halo
+    // within nine consecutive steps, while those lines are still in the XCD's
+    // L2 (tap-major, a line came back one channel sweep -- cbk steps of every
+    // tile on the XCD -- later, after the 4 MB L2 had turned over: layer4's
+    // 512 -> 512 launches fetched 1.9x the bytes they fetch now).
+    auto step_tap = [&](int s) { return s % 9; };
+    auto step_cb = [&](int s) { return s / 9; };
+#else
+    auto step_tap = [&](int s) { return s / cbk; };
+    auto step_cb = [&](int s) { return s % cbk; };
+#endif
+    // the K index (tap * cbk + cb: the weights' memory order) of step s
+    auto kidx = [&](int s) { return s < a.nmain ? step_tap(s) * cbk + step_cb(s) : s; };
     auto issue_w = [&](int s, int buf) {
         uint8_t *st = lds + buf * STAGE;
+        const int ks = kidx(s);
 #pragma unroll
-        for (int i = 0; i < NW; ++i) glds16(wr, st + (NW * wid + i) * 1024, woff[i], s * RB);
+        for (int i = 0; i < NW; ++i) glds16(wr, st + (NW * wid + i) * 1024, woff[i], ks * RB);
     };
     auto issue_x = [&](int s, int buf) {
         uint8_t *st = lds + buf * STAGE + CT * RB;
         if (a.mode2 == PV_CONV_X2_1X1 && s >= a.nmain) {
             // the 1x1 second input (the BasicBlock's downsample): centre tap at stride s2
-            const int cbo = (s - a.nmain) * RB;
+            const uint32_t cbo = (uint32_t)(s - a.nmain) * RB;
 #pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                const int q = (iy[i] * a.H2 + py[i] * a.s2) * a.W2 + px[i] * a.s2;
-                const uint32_t off = pin[i] ? (uint32_t)(q * a.Cin2 * 2 + cbo + sg16[i]) : 0x80000000u;
-                glds16(x2r, st + (NI * wid + i) * 1024, off, 0);
-            }
+            for (int i = 0; i < NI; ++i) glds16(x2r, st + (NI * wid + i) * 1024, pb2[i] + cbo, 0);
             return;
         }
-        const int tap = s / cbk, cb = s - tap * cbk;
+        const int tap = step_tap(s), cb = step_cb(s);
         const int dy = (tap / 3 - 1) * a.dil, dx = (tap % 3 - 1) * a.dil;
         const bool second = a.mode2 == PV_CONV_X2_CAT && cb >= a.cb1;   // the concatenation's second part
         const int C = second ? a.Cin2 : a.Cin, cbo = (second ? cb - a.cb1 : cb) * RB;
+        const uint32_t delta = (uint32_t)((dy * a.Win + dx) * C * 2 + cbo);
         uint32_t off[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            const int y = py[i] * a.stride + dy, x = px[i] * a.stride + dx;
-            const bool ok = pin[i] && (unsigned)y < (unsigned)a.Hin && (unsigned)x < (unsigned)a.Win;
-            off[i] = ok ? (uint32_t)(((iy[i] * a.Hin + y) * a.Win + x) * C * 2 + cbo + sg16[i]) : 0x80000000u;
+            const bool ok = (unsigned)(pyb[i] + dy) < (unsigned)a.Hin && (unsigned)(pxb[i] + dx) < (unsigned)a.Win;
+            off[i] = ok ? (second ? pb2[i] : pb1[i]) + delta : 0x80000000u;
         }
         if (second) {
 #pragma unroll
@@ -603,9 +632,19 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
 #else
         const bool nx = s + 1 < k1;
 #endif
-        if (nx) issue(s + 1, buf ^ 1);
-        compute_kc(lds + buf * STAGE, 0);
-        compute_kc(lds + buf * STAGE, 1);
+        if (PVC_ISSUE_MID == 1 || (PVC_ISSUE_MID == 2 && CT == 256)) {
+            // the next step's loads after this step's first 16 MFMAs: the MFMA
+            // pipe starts right after the barrier instead of behind every
+            // wave's address arithmetic and load issue (256-cout tiles: layer4
+            // 625-645 -> 584-630 us; the 128-cout tiles measured 4-7 % slower)
+            compute_kc(lds + buf * STAGE, 0);
+            if (nx) issue(s + 1, buf ^ 1);
+            compute_kc(lds + buf * STAGE, 1);
+        } else {
+            if (nx) issue(s + 1, buf ^ 1);
+            compute_kc(lds + buf * STAGE, 0);
+            compute_kc(lds + buf * STAGE, 1);
+        }
     }
     if (tail >= 0) {
         // Hand-off (MI355X_MICROARCH.md, "Valid forms", sc1 row): sc1

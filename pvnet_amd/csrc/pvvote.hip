@@ -3524,7 +3524,7 @@ int pv_ransac_motion_voting(const pv_image_desc *img, float *out, pv_stream_t st
 }
 
 static int evd_front(const pv_image_desc *img, const pv_vote_params *prm, void *workspace, size_t workspace_bytes,
-                     Workspace *w, int *nh, hipStream_t s) {
+                     Workspace *w, int *nh, hipStream_t s, const pv_v3_diag *diag = nullptr) {
     int r = check_desc(img);
     if (r) return r;
     if (!prm || prm->round_hyp_num <= 0 || prm->min_hyp_num <= 0) return PV_EINVAL;
@@ -3532,22 +3532,35 @@ static int evd_front(const pv_image_desc *img, const pv_vote_params *prm, void *
     *nh = rounds * prm->round_hyp_num;
     *w = carve(workspace, img->b, img->H, img->W, img->vn, *nh);
     if (!workspace || workspace_bytes < w->total) return PV_EWORKSPACE;
-    pv_v3_diag none{};
-    return front_half(img, prm, *nh, true, *w, none, s);
+    pv_v3_diag ev{};     // the diag's timing events only (bench.py's U4 line)
+    if (diag) {
+        ev.ev_vote_begin = diag->ev_vote_begin;
+        ev.ev_vote_end = diag->ev_vote_end;
+        ev.ev_compact_end = diag->ev_compact_end;
+    }
+    return front_half(img, prm, *nh, true, *w, ev, s);
+}
+
+int pv_estimate_voting_distribution_with_mean_diag(const pv_image_desc *img, const pv_vote_params *prm,
+                                                   const float *mean, float *cov, void *workspace,
+                                                   size_t workspace_bytes, const pv_v3_diag *diag,
+                                                   pv_stream_t stream) {
+    if (!mean || !cov) return PV_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    Workspace w;
+    int nh = 0;
+    int r = evd_front(img, prm, workspace, workspace_bytes, &w, &nh, s, diag);
+    if (r) return r;
+    k_evd_with_mean<<<dim3(img->vn, img->b), 256, 0, s>>>(w.counts, w.hyp, w.fgtot, w.tn, img->vn, nh, prm->min_num,
+                                                          prm->min_hyp_num, mean, cov);
+    return last();
 }
 
 int pv_estimate_voting_distribution_with_mean(const pv_image_desc *img, const pv_vote_params *prm,
                                               const float *mean, float *cov, void *workspace,
                                               size_t workspace_bytes, pv_stream_t stream) {
-    if (!mean || !cov) return PV_EINVAL;
-    hipStream_t s = (hipStream_t)stream;
-    Workspace w;
-    int nh = 0;
-    int r = evd_front(img, prm, workspace, workspace_bytes, &w, &nh, s);
-    if (r) return r;
-    k_evd_with_mean<<<dim3(img->vn, img->b), 256, 0, s>>>(w.counts, w.hyp, w.fgtot, w.tn, img->vn, nh, prm->min_num,
-                                                          prm->min_hyp_num, mean, cov);
-    return last();
+    return pv_estimate_voting_distribution_with_mean_diag(img, prm, mean, cov, workspace, workspace_bytes, nullptr,
+                                                          stream);
 }
 
 int pv_estimate_voting_distribution(const pv_image_desc *img, const pv_vote_params *prm, float *mean, float *cov,

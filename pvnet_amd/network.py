@@ -12,8 +12,11 @@ Module tree and state-dict keys are those of ``PVnet``
   -> conv2s(cat[., x2s]) -> up x2 -> convraw(cat[., image]) -> 1x1 -> seg 2 + vertex 2K
 
 Upsampling is ``UpsamplingBilinear2d`` (align_corners=True) as in MR:35,43,51.
-The convolutions run through MIOpen; ``channels_last`` and fp16/bf16 autocast
-are the MI355X knobs (the reference's fp16 precedent:
+The module form :class:`PVNet` runs its convolutions through MIOpen; the
+inference form :class:`PVNetInference` runs every fp16 convolution (with its
+epilogue) as one of this repository's HIP matrix-core kernels
+(``pvnet_amd/csrc/pvconv.hip``) and, in f32, MIOpen + HIP epilogue passes.
+``channels_last`` and fp16 are the MI355X knobs (the reference's fp16 precedent:
 python-only-xin/pvnet-master/tools/train_linemod.py:514).  No weights ship with
 the reference (README.md:101 points to a download), so the default init is the
 reference's own (RN:156-163: He-normal convs, BN weight 1 / bias 0).
@@ -21,7 +24,7 @@ reference's own (RN:156-163: He-normal convs, BN weight 1 / bias 0).
 from __future__ import annotations
 
 import math
-
+import threading
 
 import torch
 import torch.nn.functional as F
@@ -400,12 +403,14 @@ def conv3x3(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, dil: int, act:
 
 
 _CONV_WS: dict = {}
+_CONV_WS_LOCK = threading.Lock()     # per-GPU threads (DataParallel-style callers) share the table
 
 
 def clear_conv_workspaces() -> None:
     """Drop every split-K scratch buffer (no captured graph that used one may
     be replayed afterwards)."""
-    _CONV_WS.clear()
+    with _CONV_WS_LOCK:
+        _CONV_WS.clear()
 
 CONV_SPLIT = True          # the split-K last round (A/B hook for tools/backbone_ab2.py; no environment switch)
 
@@ -414,20 +419,27 @@ def _conv_workspace(x: torch.Tensor, pixels: int, cout: int, ksteps: int):
     """The split-K scratch of pv_conv3x3_ex_f16 (its last partial round of
     tiles): one buffer per (device, stream), since calls on one stream run in
     order; grown to the largest need and kept, so a captured graph keeps
-    using the buffer it captured (a buffer first made during a capture comes
-    from the graph's pool).  A process that keeps creating streams should
-    call :func:`clear_conv_workspaces` once their graphs are gone.
+    using the buffer it captured.  Its arrival counters must start at zero,
+    so buffers are only made (zero-filled) outside a stream capture: inside
+    one, a call with no large enough buffer runs without split-K (ws NULL)
+    rather than take memory whose zero fill would only run at replay.  A
+    process that keeps creating streams should call
+    :func:`clear_conv_workspaces` once their graphs are gone.
     (pointer, bytes) or (None, 0)."""
     from pvnet_amd import _lib
     need = int(_lib.load().pv_conv3x3_workspace_bytes(pixels, cout, ksteps))
     if need <= 0 or not CONV_SPLIT:
         return None, 0
     key = (x.device, torch.cuda.current_stream(x.device).cuda_stream)
-    bufs = _CONV_WS.setdefault(key, [])
-    if not bufs or bufs[-1].numel() < need:
-        # a smaller buffer is kept alive too: a graph captured with it still uses it
-        bufs.append(torch.zeros(need, dtype=torch.uint8, device=x.device))   # zeroed once (pvvote.h)
-    return bufs[-1].data_ptr(), bufs[-1].numel()
+    capturing = torch.cuda.is_current_stream_capturing()
+    with _CONV_WS_LOCK:
+        bufs = _CONV_WS.setdefault(key, [])
+        if not bufs or bufs[-1].numel() < need:
+            if capturing:
+                return None, 0
+            # a smaller buffer is kept alive too: a graph captured with it still uses it
+            bufs.append(torch.zeros(need, dtype=torch.uint8, device=x.device))   # zeroed once (pvvote.h)
+        return bufs[-1].data_ptr(), bufs[-1].numel()
 
 
 def conv3x3_weight(c: nn.Conv2d, ds: nn.Conv2d | None = None) -> torch.Tensor:
@@ -697,7 +709,7 @@ class PVNetInference(nn.Module):
         pool3 = (mp.kernel_size, mp.stride, mp.padding, mp.dilation, mp.ceil_mode) == (3, 2, 1, 1, False)
         if (self.fused_conv and x.dtype == torch.float16 and stem_eligible(r.conv1) and x.shape[2] % 2 == 0
                 and x.shape[3] % 2 == 0):
-            key = (r.conv1.weight.data_ptr(), r.conv1.weight._version, r.conv1.bias.data_ptr())
+            key = (r.conv1.weight.data_ptr(), r.conv1.weight._version, r.conv1.bias.data_ptr(), r.conv1.bias._version)
             if getattr(self, "_stem_key", None) != key:     # the kernel's weight layout, made once
                 self._stem_w = stem_weights(r.conv1)
                 self._stem_key = key
@@ -738,7 +750,7 @@ class PVNetInference(nn.Module):
         c4 = self.conv4s[0]
         if (fm.dtype == torch.float16 and self.fused_conv and fm.shape[1] == 128 and x4s.shape[1] == 64
                 and c4.in_channels == 192 and c4.out_channels == 64 and c4.kernel_size == (3, 3)):
-            key = (c4.weight.data_ptr(), c4.weight._version, c4.bias.data_ptr())
+            key = (c4.weight.data_ptr(), c4.weight._version, c4.bias.data_ptr(), c4.bias._version)
             if getattr(self, "_c4s_key", None) != key:
                 self._c4s_w = decoder_conv4s_weights(c4)
                 self._c4s_key = key
@@ -749,7 +761,7 @@ class PVNetInference(nn.Module):
         c2 = self.conv2s[0]
         if (fm.dtype == torch.float16 and self.fused_conv and fm.shape[1] == 64 and x2s.shape[1] == 64
                 and c2.in_channels == 128 and c2.out_channels == 32 and c2.kernel_size == (3, 3)):
-            key = (c2.weight.data_ptr(), c2.weight._version, c2.bias.data_ptr())
+            key = (c2.weight.data_ptr(), c2.weight._version, c2.bias.data_ptr(), c2.bias._version)
             if getattr(self, "_c2s_key", None) != key:     # the kernel's weight layout, made once
                 self._c2s_w = decoder_conv2s_weights(c2)
                 self._c2s_key = key
@@ -760,14 +772,21 @@ class PVNetInference(nn.Module):
         c0, c1 = self.convraw[0], self.convraw[3]
         slope = self.convraw[2].negative_slope
         if x.dtype == torch.float16 and self.fused_tail:
-            key = (c0.weight.data_ptr(), c0.bias.data_ptr(), c1.weight.data_ptr(), c1.bias.data_ptr())
+            key = (c0.weight.data_ptr(), c0.weight._version, c0.bias.data_ptr(), c0.bias._version,
+                   c1.weight.data_ptr(), c1.weight._version, c1.bias.data_ptr(), c1.bias._version)
             if getattr(self, "_tail_key", None) != key:     # matrix-core layouts of convraw's weights, made once
                 self._tail_w = decoder_tail_weights(c0, c1, self.raw_in)
                 self._tail_key = key
             out = decoder_tail(fm, x, self._tail_w, slope)
             return out[:, :self.seg_dim], out[:, self.seg_dim:]
         fm = upsample2x_cat(fm, x, self.raw_pad)
-        key = (c0.bias.data_ptr(), c1.weight.data_ptr(), c1.bias.data_ptr(), c1.weight.dtype)
+        if not (c0.out_channels == 32 and c1.out_channels in (20, 44)):
+            # pv_head_f16/_f32 take 32 -> 20 / 44 (the reference's two heads); other
+            # PVNet(ver_dim, seg_dim, raw_dim) shapes run convraw's modules
+            out = self.convraw(fm)
+            return out[:, :self.seg_dim], out[:, self.seg_dim:]
+        key = (c0.bias.data_ptr(), c0.bias._version, c1.weight.data_ptr(), c1.weight._version, c1.bias.data_ptr(),
+               c1.bias._version, c1.weight.dtype)
         if getattr(self, "_head_key", None) != key:     # f32 copies of the head's parameters, made once
             self._head_w = (c0.bias.detach().float().contiguous(),
                             c1.weight.detach().float().reshape(c1.out_channels, -1).contiguous(),

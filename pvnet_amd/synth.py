@@ -50,6 +50,13 @@ def synthetic_field(seed=1234, H=480, W=640, vn=9, radius=97.5, center=(320.0, 2
     return dict(seg=seg, vertex=vertex, mask=m, keypoints=kps, tn=tn)
 
 
+def field_keypoints(seed=1234, vn=9):
+    """The keypoints of S(seed) (synthetic_field's first draw) without
+    building the field: lets a rank check the stream order of images it never
+    held."""
+    return np.random.default_rng(seed).uniform([200.0, 120.0], [440.0, 360.0], size=(vn, 2))
+
+
 STREAM_KINDS = ("full", "split", "tiny", "large", "corner", "empty", "border", "small")
 
 

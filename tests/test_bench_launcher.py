@@ -1,0 +1,55 @@
+"""bench.py's own multi-rank launch (`python bench.py --gpus N` outside torchrun)
+on CPU: the parent starts N gloo ranks (bench.launch_ranks), they shard the
+stream, gather it, take the max time over ranks, and rank 0 prints ONE JSON
+line with n_gpus == N, a verified stream order and the CPU baseline.  The
+--dry-run flag replaces the voting by the fields' generating keypoints (the
+product path needs a GPU), everything around it is the real run's code."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*extra, env_extra=None, timeout=240):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--dry-run", "--steps", "3", "--warmup", "1",
+           "--per-step", "10", "--fields", "4", "--cpu-seconds", "1"] + list(extra)
+    return subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_launcher_gpus_n_gloo(n):
+    p = _run("--gpus", str(n))
+    assert p.returncode == 0, p.stderr[-3000:]
+    # one JSON line, from rank 0 only (gloo itself prints a connection note)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == n and line["dry_run"] is True
+    assert line["stream_order_ok"] and line["stream_order_max_err_px"] == 0.0
+    assert line["config"]["stream_images"] == n * 3 * 10
+    assert line["cpu_baseline"]["value"] > 0          # rank 0 reports it at every N
+
+
+def test_launcher_gpus_1_single_process():
+    p = _run("--gpus", "1", "--skip-cpu")
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert line["n_gpus"] == 1 and line["stream_order_ok"]
+
+
+def test_world_size_mismatch_fails():
+    p = _run("--gpus", "2", "--skip-cpu", env_extra={"WORLD_SIZE": "1", "RANK": "0"})
+    assert p.returncode != 0 and "WORLD_SIZE 1 != --gpus 2" in p.stderr
+
+
+def test_failing_rank_stops_launch():
+    # ranks that raise (an empty stream: nothing to stack) make the launcher
+    # stop the others and return non-zero instead of waiting
+    p = _run("--gpus", "2", "--skip-cpu", "--steps", "0")
+    assert p.returncode != 0
