@@ -198,38 +198,32 @@ def make_stream_fields(rank, ws, nfields, dev):
     return segs, vers, np.stack(kps), np.array(tns), kinds
 
 
-def run_stream(args, ws, rank, dev, segs, vers, steps, seed_base):
-    """The timed stream: this rank's share (pvnet_amd.distributed.shard) of
-    ws * steps * per_step batch-1 frames, each a ransac_voting_layer_v3 call
-    on seg_pred/vertex_pred of resident field j % len(segs); one step = one
-    hipGraph replay of per_step calls, --inflight of them at a time on their
-    own streams and workspaces; one gather of every keypoint at the end.
-    Returns (elapsed s (max over ranks), local keypoints [steps*M, 9, 2],
-    lanes' workspaces, the capture stream)."""
+def graph_stream(args, ws, rank, dev, steps, seed_base, vote, parts, per_step=None, lanes_state=None):
+    """The timed stream core: this rank's share (pvnet_amd.distributed.shard)
+    of ws * steps * M images; one step = one hipGraph replay of M calls of
+    ``vote(j, seed, lane, outs)`` (slot j writes row j of each per-step output
+    in ``outs``), --inflight of them at a time on their own streams; one
+    gather of every image's result at the end of the timed region.
+    ``parts`` = [(shape, dtype)] of one image's result.  Returns (elapsed s
+    (max over ranks), local results [steps*M, ...] per part, gathered
+    results per part (stream order), the capture stream)."""
     from pvnet_amd import distributed as D
-    from pvnet_amd import ransac_voting_gpu as rvg
-    M, K, NF = args.per_step, steps, len(segs)
+    M, K = per_step or args.per_step, steps
     n_images = ws * K * M                          # the whole stream, sharded round-robin (SURVEY 8(e))
     mine = D.shard(n_images, rank, ws)             # this rank's images, in stream order
     assert len(mine) == K * M
     NL = max(1, args.inflight)
     lanes = [torch.cuda.Stream(device=dev) for _ in range(NL)]
-    works = [rvg.VotingWorkspace() for _ in range(NL)]
-    out_step = torch.zeros((M, VN, 2), dtype=torch.float32, device=dev)
-    local = torch.zeros((K * M, VN, 2), dtype=torch.float32, device=dev)
+    outs = [torch.zeros((M,) + tuple(sh), dtype=dt, device=dev) for sh, dt in parts]
+    local = [torch.zeros((K * M,) + tuple(sh), dtype=dt, device=dev) for sh, dt in parts]
     s = torch.cuda.Stream(device=dev)
-
-    def vote(j, seed):
-        # slot j of a step: lane j % NL (its own stream and workspace), field j % NF
-        with torch.cuda.stream(lanes[j % NL]):
-            rvg.ransac_voting_layer_v3_from_network(segs[j % NF], vers[j % NF], args.hn, _seed=seed,
-                                                   _workspace=works[j % NL], out=out_step[j:j + 1])
 
     def step_body(seed0):
         for ln in lanes:
             ln.wait_stream(torch.cuda.current_stream())
         for j in range(M):
-            vote(j, seed0 + 17 * j)
+            with torch.cuda.stream(lanes[j % NL]):
+                vote(j, seed0 + 17 * j, j % NL, outs)
         for ln in lanes:
             torch.cuda.current_stream().wait_stream(ln)
 
@@ -252,10 +246,14 @@ def run_stream(args, ws, rank, dev, segs, vers, steps, seed_base):
     with torch.cuda.stream(s):
         for k in range(K):
             graph.replay()
-            local[k * M:(k + 1) * M].copy_(out_step)
-        # the stream's one exchange: keypoints of every image to every rank, in
+            for loc, o in zip(local, outs):
+                loc[k * M:(k + 1) * M].copy_(o)
+        # the stream's one exchange: every image's result to every rank, in
         # stream order (pvnet_amd.distributed: RCCL all_gather over xGMI)
-        allkp = D.gather_results(local, n_images, rank, ws)
+        if len(parts) == 1:
+            allr = (D.gather_results(local[0], n_images, rank, ws),)
+        else:
+            allr = D.gather_results_multi(local, n_images, rank, ws)
     torch.cuda.synchronize()
     if ws > 1:
         dist.barrier()
@@ -265,8 +263,26 @@ def run_stream(args, ws, rank, dev, segs, vers, steps, seed_base):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         mine_t = torch.tensor(mine, device=dev)
-        assert torch.equal(allkp[mine_t], local), "gathered stream order differs from the shard"
-    return elapsed, local, works, s, allkp
+        for a_, l_ in zip(allr, local):
+            assert torch.equal(a_[mine_t], l_), "gathered stream order differs from the shard"
+    return elapsed, local, allr, s
+
+
+def run_stream(args, ws, rank, dev, segs, vers, steps, seed_base):
+    """The v3 stream: ransac_voting_layer_v3 on seg_pred/vertex_pred of
+    resident field j % len(segs) per slot, its own workspace per lane.
+    Returns (elapsed s (max over ranks), local keypoints [steps*M, 9, 2],
+    lanes' workspaces, the capture stream, gathered keypoints)."""
+    from pvnet_amd import ransac_voting_gpu as rvg
+    NF = len(segs)
+    works = [rvg.VotingWorkspace() for _ in range(max(1, args.inflight))]
+
+    def vote(j, seed, lane, outs):
+        rvg.ransac_voting_layer_v3_from_network(segs[j % NF], vers[j % NF], args.hn, _seed=seed,
+                                               _workspace=works[lane], out=outs[0][j:j + 1])
+    elapsed, local, allr, s = graph_stream(args, ws, rank, dev, steps, seed_base, vote,
+                                           [((VN, 2), torch.float32)])
+    return elapsed, local[0], works, s, allr[0]
 
 
 def stream_order_error(allkp, ws, nfields):
@@ -355,9 +371,10 @@ def main():
 
     # configs[3]: the Occlusion-LINEMOD-like stream (mixed masks), the same
     # sharding and gather, fewer steps
-    c3 = None
+    c3 = c4 = None
     if not args.skip_config3:
         c3 = stream_config3(args, ws, rank, dev)
+        c4 = stream_config4(args, ws, rank, dev)
 
     # dominant kernels' durations with hipEvents on the streams they run on
     seeds = [rank * 1_000_003 + 17 * k + 3 for k in range(min(K * 5, 100))]
@@ -377,7 +394,7 @@ def main():
     torch.cuda.synchronize()
     latency_ms = (time.perf_counter() - t1) / NLAT * 1e3
     res = dict(elapsed=elapsed, vote_ms=vote_ms, compact_ms=compact_ms, tn=tn, latency_ms=latency_ms,
-               n_images=n_images, config3=c3, order_err=order_err)
+               n_images=n_images, config3=c3, config4=c4, order_err=order_err)
     if rank == 0:
         report(args, ws, res, err, dev)
     if ws > 1:
@@ -415,6 +432,83 @@ def stream_config3(args, ws, rank, dev, steps=8):
                      "max_num (Bernoulli downsampling, RV:543-546) / quadrant-occluded / empty / border-clipped / "
                      "just above min_num frames cycling, images sharded round-robin over ranks, one all_gather of "
                      "keypoints; parity: tests/test_gpu_stream.py")
+
+
+YCB_K = np.array([[1066.778, 0.0, 312.9869], [0.0, 1067.487, 241.3109], [0.0, 0.0, 1.0]])   # the YCB-Video camera
+
+
+def make_ycb_fields(rank, ws, nfields, dev, kp=21):
+    """The rank's resident configs[4] frames: 21 model points (a seeded
+    12 cm object) at a random pose 0.9-1.1 m in front of the YCB camera,
+    projected to 21 keypoints; S(seed)-style field around them (disk r 97.5,
+    ~29.9k foreground pixels, 0.05 rad noise, 20 % outliers), network layout
+    f32.  Returns (segs, vers, model points, poses [nf, 3, 4])."""
+    from pvnet_amd import synth
+    p3 = np.random.default_rng(5).uniform(-0.06, 0.06, size=(kp, 3))
+    segs, vers, poses = [], [], []
+    for f_ in range(nfields):
+        rng = np.random.default_rng(90_000 + rank + ws * f_)
+        a = rng.normal(size=3) * 0.4
+        th = np.linalg.norm(a)
+        kx = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]]) / th
+        R = np.eye(3) + np.sin(th) * kx + (1 - np.cos(th)) * kx @ kx
+        t = np.array([rng.uniform(-0.05, 0.05), rng.uniform(-0.05, 0.05), rng.uniform(0.9, 1.1)])
+        X = p3 @ R.T + t
+        k2 = np.stack([YCB_K[0, 0] * X[:, 0] / X[:, 2] + YCB_K[0, 2], YCB_K[1, 1] * X[:, 1] / X[:, 2] + YCB_K[1, 2]], 1)
+        fd = synth.synthetic_field(90_000 + rank + ws * f_, vn=kp, keypoints=k2,
+                                   center=(float(k2[:, 0].mean()), float(k2[:, 1].mean())))
+        segs.append(torch.from_numpy(fd["seg"]).to(dev))
+        vers.append(torch.from_numpy(fd["vertex"]).to(dev))
+        poses.append(np.concatenate([R, t[:, None]], 1))
+    return segs, vers, p3, np.stack(poses)
+
+
+def stream_config4(args, ws, rank, dev, steps=4, per_step=32, nfields=16):
+    """configs[4] (BASELINE.json): the YCB-Video stream sharded round-robin
+    over the ranks; per image ransac_voting_layer_v3 (hn 512) from the
+    network layout, estimate_voting_distribution_with_mean (16 x 256
+    hypotheses) on argmax(seg) and the strided vertex view, and the
+    uncertainty PnP of the 21 keypoints; one gather of (keypoints [21, 2],
+    covariances [21, 2, 2], pose [3, 4]) per image in stream order.  Same
+    graph-replayed lanes as the headline stream; images/s over all ranks."""
+    from pvnet_amd import extend_utils as eu
+    from pvnet_amd import ransac_voting_gpu as rvg
+    KP = 21
+    segs, vers, p3, poses = make_ycb_fields(rank, ws, nfields, dev, KP)
+    tp3 = torch.from_numpy(p3).to(dev)
+    tK = torch.from_numpy(YCB_K).to(dev)
+    NL = max(1, args.inflight)
+    w1 = [rvg.VotingWorkspace() for _ in range(NL)]
+    w2 = [rvg.VotingWorkspace() for _ in range(NL)]
+
+    def vote(j, seed, lane, outs):
+        seg, ver = segs[j % nfields], vers[j % nfields]
+        b, c, h, w = ver.shape
+        kp = rvg.ransac_voting_layer_v3_from_network(seg, ver, args.hn, _seed=seed, _workspace=w1[lane],
+                                                     out=outs[0][j:j + 1])
+        mask = seg.argmax(1)
+        vertex = ver.permute(0, 2, 3, 1).view(b, h, w, KP, 2)
+        mean, cov = rvg.estimate_voting_distribution_with_mean(mask, vertex, kp, _workspace=w2[lane], _seed=seed + 1)
+        outs[1][j:j + 1].copy_(cov)
+        outs[2][j:j + 1].copy_(eu.pose_from_voting(mean, cov, tp3, tK))
+    parts = [((KP, 2), torch.float32), ((KP, 2, 2), torch.float32), ((3, 4), torch.float64)]
+    elapsed, local, allr, _ = graph_stream(args, ws, rank, dev, steps, 70_000, vote, parts, per_step=per_step)
+    n = ws * steps * per_step
+    Rt = local[2].cpu().numpy()
+    j = np.arange(Rt.shape[0]) % nfields
+    terr = np.abs(Rt[:, :, 3] - poses[j][:, :, 3]).max(1)
+    del segs, vers
+    torch.cuda.empty_cache()
+    return dict(images_per_s=round(n / elapsed, 1), ms_per_step=round(elapsed / steps * 1e3, 4), steps=steps,
+                per_gpu_batch_per_step=per_step, n_gpus=ws, stream_images=n, keypoints=KP,
+                gathered=[list(a.shape) for a in allr],
+                covariances_finite=bool(torch.isfinite(local[1]).all()),
+                max_translation_err_m=round(float(terr.max()), 5), median_translation_err_m=round(float(np.median(terr)), 5),
+                stages="v3 (hn 512) + EVD with mean (16 x 256) + uncertainty PnP (21 points) per image, graph-replayed "
+                       "lanes; (keypoints, covariances, pose) gathered in stream order",
+                note="configs[4] workload: YCB-Video-like 480x640 frames (21 keypoints of a 12 cm object 0.9-1.1 m "
+                     "from the YCB camera, ~29.9k foreground px), images sharded round-robin over ranks; error vs "
+                     "the generating pose; parity: tests/test_gpu_stream.py::test_config4_stream_*")
 
 
 def time_vote_kernel(rvg, segs, vers, hn, seeds, work, out, stream):
@@ -1008,6 +1102,8 @@ def report(args, ws, res, final_err, dev):
     }
     if res.get("config3") is not None:
         line["stream_config3"] = res["config3"]
+    if res.get("config4") is not None:
+        line["stream_config4"] = res["config4"]
     try:
         line["kp_err_vs_ref_px"] = measure_kp_vs_ref(dev)
     except Exception as e:

@@ -452,10 +452,114 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_ba
 #ifndef PVC_CB_MAJOR
 #define PVC_CB_MAJOR 1
 #endif
+#ifndef PVC_WINDOW
+#define PVC_WINDOW 0             // 1: stride-1 convolutions on k_conv3x3w (A/B variant; measured slower)
+#endif
 #ifndef PVC_ISSUE_MID
 #define PVC_ISSUE_MID 2          // 0 before the step's MFMAs, 1 after its first half, 2 = 1 for 256-cout tiles only
 #endif
 constexpr int kNW = PVC_NW;                   // waves per block: 16 (4 cout x 4 pixel groups; 8 = 2 x 4 measured 5-8 % slower)
+
+// The end of a k_conv3x3 / k_conv3x3w tile: a split tile's part hands its
+// f32 partials over (the last part to arrive sums them in part order), then
+// the epilogue (bias, residual (+ its bias), activation; k_epilogue's
+// roundings) and the channels-last stores.
+template <int CT, int MI, int WC>
+__device__ __forceinline__ void conv_finish(const ConvArgs &a, f4v (&acc)[MI][4], int tail, int part, int n0,
+                                            int64_t p0, int wn, int wm, int lane, uint8_t *lds) {
+    if (tail >= 0) {
+        // Hand-off (MI355X_MICROARCH.md, "Valid forms", sc1 row): sc1
+        // (write-through) partial stores, every wave's vmcnt(0), a barrier,
+        // one agent-scope ticket add; the last arriver reads every other
+        // part's partials with sc1 loads.
+        constexpr int NF = MI * 4;                    // 16-byte accumulator groups per thread
+        const int64_t slab_bytes = (int64_t)a.nsplit * NF * (64 * kNW) * 16;
+        const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)((uint8_t *)a.slab + (int64_t)tail * slab_bytes), 0, (int)slab_bytes, 0x00020000);
+        const int tbase = (int)threadIdx.x * 16;
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+                const int f = mi * 4 + ni;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, acc[mi][ni]), sr,
+                                                       ((part * NF + f) * (64 * kNW)) * 16 + tbase, 0, 16);
+            }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int *flag = (int *)lds;                       // the stages are free: the loop's reads are done
+        if (threadIdx.x == 0) {
+            const int t = __hip_atomic_fetch_add(&a.tick[tail], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            flag[0] = t == a.nsplit - 1;
+        }
+        __syncthreads();
+        if (!flag[0]) return;
+        if (threadIdx.x == 0) a.tick[tail] = 0;       // zero again for the next call on this ws
+        // every part's partials from the slabs (this block's own included), in
+        // part order: the sum does not depend on which part arrived last, and
+        // the accumulators are reused (no second register set)
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+                const int f = mi * 4 + ni;
+                f4v t = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(sr, f * (64 * kNW) * 16 + tbase, 0, 16));
+                for (int p = 1; p < a.nsplit; ++p)
+                    t += __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     sr, ((p * NF + f) * (64 * kNW)) * 16 + tbase, 0, 16));
+                acc[mi][ni] = t;
+            }
+    }
+    // ---- epilogue: lane's accumulator (mi, ni) = couts c .. c+3 of pixel p;
+    // k_epilogue's roundings (bias add, residual (+ its bias), activation) ----
+    h4 bq[MI], rbq[MI];
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+        const int c = n0 + wn * (MI * 16) + mi * 16 + 4 * (lane >> 4);
+        bq[mi] = *(const h4 *)(a.bias + c);
+        rbq[mi] = a.rbias ? *(const h4 *)(a.rbias + c) : h4{};
+    }
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+        const int64_t p = p0 + wm * 64 + ni * 16 + (lane & 15);
+        const bool pv = p < a.M;
+        const int64_t pc = pv ? p : 0;
+        h4 r[MI];
+        if (a.res) {
+#pragma unroll
+            for (int mi = 0; mi < MI; ++mi)
+                r[mi] = *(const h4 *)(a.res + pc * a.Cout + n0 + wn * (MI * 16) + mi * 16 + 4 * (lane >> 4));
+        }
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) {
+            const int c = n0 + wn * (MI * 16) + mi * 16 + 4 * (lane >> 4);
+            h4 y;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) y[j] = (_Float16)((float)(_Float16)acc[mi][ni][j] + (float)bq[mi][j]);
+            if (a.res) {
+                h4 rr = r[mi];
+                if (a.rbias) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) rr[j] = (_Float16)((float)rr[j] + (float)rbq[mi][j]);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) y[j] = (_Float16)((float)y[j] + (float)rr[j]);
+            } else if (a.rbias) {
+                // the downsample's bias (its convolution summed in the accumulator)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) y[j] = (_Float16)((float)y[j] + (float)rbq[mi][j]);
+            }
+            if (a.act == 1) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) y[j] = (float)y[j] > 0.f ? y[j] : (_Float16)0.f;
+            } else if (a.act == 2) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) y[j] = (float)y[j] > 0.f ? y[j] : (_Float16)((float)y[j] * a.slope);
+            }
+            if (pv) *(h4 *)(a.out + p * a.ldo + c) = y;
+        }
+    }
+}
 
 template <int CT>
 __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
@@ -626,6 +730,9 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
     for (int s = k0; s < k1; ++s) {
         const int buf = (s - k0) & 1;
         __builtin_amdgcn_s_waitcnt(0x0F70);          // this wave's loads of step s have landed (vmcnt 0)
+#ifdef PVC_NO_BARRIER
+        if (s == k0)
+#endif
         __syncthreads();                              // ... and every wave's; step s-1's reads are done
 #ifdef PVC_NO_LOADS
         const bool nx = s == k0 && k1 - k0 > 1;
@@ -646,99 +753,213 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
             compute_kc(lds + buf * STAGE, 1);
         }
     }
-    if (tail >= 0) {
-        // Hand-off (MI355X_MICROARCH.md, "Valid forms", sc1 row): sc1
-        // (write-through) partial stores, every wave's vmcnt(0), a barrier,
-        // one agent-scope ticket add; the last arriver reads every other
-        // part's partials with sc1 loads.
-        constexpr int NF = MI * 4;                    // 16-byte accumulator groups per thread
-        const int64_t slab_bytes = (int64_t)a.nsplit * NF * (64 * kNW) * 16;
-        const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)((uint8_t *)a.slab + (int64_t)tail * slab_bytes), 0, (int)slab_bytes, 0x00020000);
-        const int tbase = (int)threadIdx.x * 16;
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < 4; ++ni) {
-                const int f = mi * 4 + ni;
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, acc[mi][ni]), sr,
-                                                       ((part * NF + f) * (64 * kNW)) * 16 + tbase, 0, 16);
-            }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        int *flag = (int *)lds;                       // the stages are free: the loop's reads are done
-        if (threadIdx.x == 0) {
-            const int t = __hip_atomic_fetch_add(&a.tick[tail], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            flag[0] = t == a.nsplit - 1;
-        }
-        __syncthreads();
-        if (!flag[0]) return;
-        if (threadIdx.x == 0) a.tick[tail] = 0;       // zero again for the next call on this ws
-        // every part's partials from the slabs (this block's own included), in
-        // part order: the sum does not depend on which part arrived last, and
-        // the accumulators are reused (no second register set)
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < 4; ++ni) {
-                const int f = mi * 4 + ni;
-                f4v t = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(sr, f * (64 * kNW) * 16 + tbase, 0, 16));
-                for (int p = 1; p < a.nsplit; ++p)
-                    t += __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(
-                                                     sr, ((p * NF + f) * (64 * kNW)) * 16 + tbase, 0, 16));
-                acc[mi][ni] = t;
-            }
+    conv_finish<CT, MI, WC>(a, acc, tail, part, n0, p0, wn, wm, lane, lds);
+}
+
+
+// --------------------------------------------------------------------------
+// The window form (stride 1, dilation <= kMaxDil): the same tiles, K order
+// (channel block, ky, kx) and epilogue as k_conv3x3, but a tile's pixel
+// operand for the three taps of one kernel row ky comes from ONE window of
+// 256 + 2d consecutive pixels (the tile's, shifted by the row offset dy and
+// widened by d on both sides) staged once in LDS: tap kx reads the window's
+// rows shifted by (kx - 1) d, and the lanes whose pixel x + dx leaves its
+// image row (where the linear shift wraps into the next row) take zeros, the
+// convolution's padding.  A step's loads drop from 32 KiB of weights + 32 KiB
+// of pixels to 32 KiB + a third of a 33 KiB window (layer4: ~2/3 of the
+// bytes, and 2 + 1 instead of 4 LDS-DMA pieces per wave and step).  A
+// window's 33 pieces are issued in thirds during the three steps of the
+// window before it; the downsample's 1x1 steps (PV_CONV_X2_1X1) are
+// one-step windows of the tile's own 256 pixels.
+// LDS: 2 weight stages (CT rows x 128 B) + 2 windows (264 rows x 128 B).
+// Measured (round 4, tools/r04_gpu5.sh): correct (the conv3x3 parity cases)
+// but slower than k_conv3x3 on every layer (layer4 640-690 against 583-630
+// us): the kernel is not bound by its bytes; the masking and the longer
+// path from the barrier to the first MFMA cost more than the loads saved.
+// Kept as an A/B build (PVC_WINDOW=1), not in the product library.
+// --------------------------------------------------------------------------
+#if PVC_WINDOW
+constexpr int kMaxDil = 4;
+constexpr int kWinRows = kPT + 2 * kMaxDil;          // 264
+constexpr int kWinPieces = kWinRows * 128 / 1024;    // 33 LDS-DMA pieces (1 KiB) per window
+constexpr int kWinThird = (kWinPieces + 2) / 3;      // 11: pieces per step, one per wave 0..10
+
+template <int CT>
+__global__ __launch_bounds__(64 * kNW) void k_conv3x3w(ConvArgs a) {
+    constexpr int RB = 128;                                // bytes per LDS row (64 channels)
+    constexpr int GPR = RB / 16;
+    constexpr int WST = CT * RB;                           // weight stage: 32 KiB (CT 256)
+    constexpr int XST = kWinRows * RB;                     // window: 33 KiB
+    constexpr int NW = (CT * RB) / (1024 * kNW);           // weight pieces per wave per step
+    constexpr int WC = kNW / 4;
+    constexpr int MI = CT / WC / 16;
+    static_assert(kWinThird <= kNW, "one window piece per wave and step");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WST + 2 * XST];
+    const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
+    int bid = (int)blockIdx.x, part = 0, tail = -1;
+    if (bid < a.nfull) {
+        const int nb = a.nfull, q = nb / 8, r = nb % 8, x = bid % 8;
+        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+    } else {
+        const int j = bid - a.nfull;
+        tail = j / a.nsplit;
+        part = j - tail * a.nsplit;
+        bid = a.nfull + tail;
     }
-    // ---- epilogue: lane's accumulator (mi, ni) = couts c .. c+3 of pixel p;
-    // k_epilogue's roundings (bias add, residual (+ its bias), activation) ----
-    h4 bq[MI], rbq[MI];
+    const int ct = bid % a.nct, pt = bid / a.nct;
+    const int n0 = ct * CT;
+    const int64_t p0 = (int64_t)pt * kPT;
+    const int d = a.dil;
+    const __amdgpu_buffer_rsrc_t wr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.w, 0, (int)((int64_t)a.Cout * a.ksteps * 128), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)a.x, 0, (int)((int64_t)a.N * a.H * a.W * a.Cin * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t x2r = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)a.x2, 0,
+        a.mode2 == PV_CONV_X2_1X1 ? (int)((int64_t)a.N * a.H2 * a.W2 * a.Cin2 * 2)
+                                  : (int)((int64_t)a.N * a.H * a.W * a.Cin2 * 2),
+        0x00020000);
+    const int K2 = a.ksteps * RB;
+    const int cbk = a.cblocks;
+    const int64_t HW = (int64_t)a.H * a.W;
+    int woff[NW];
 #pragma unroll
-    for (int mi = 0; mi < MI; ++mi) {
-        const int c = n0 + wn * (MI * 16) + mi * 16 + 4 * (lane >> 4);
-        bq[mi] = *(const h4 *)(a.bias + c);
-        rbq[mi] = a.rbias ? *(const h4 *)(a.rbias + c) : h4{};
+    for (int i = 0; i < NW; ++i) {
+        const int g = (NW * wid + i) * 64 + lane, row = g / GPR, pseg = g % GPR;
+        woff[i] = (n0 + row) * K2 + (pseg ^ (row & 7)) * 16;
     }
+    // this lane's window granules: piece u * kWinThird + wid (u = 0..2, waves
+    // 0..10), row = piece * 8 + lane / 8, segment (lane & 7) ^ (row & 7); for
+    // the 3x3 windows the pixel q = p0 - d + row (its index and row y, or far
+    // out of range past the window / the map), for the 1x1 windows the byte
+    // offset of pixel p0 + row's input in x2
+    const uint32_t seg16 = (uint32_t)(((lane & 7) ^ (lane >> 3)) * 16);
+    int qpix[3], qy[3];
+    uint32_t qds[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+        const int piece = u * kWinThird + wid, row = piece * 8 + (lane >> 3);
+        const int64_t q = p0 - d + row;
+        const bool in = wid < kWinThird && piece < kWinPieces && row < kPT + 2 * d && q >= 0 && q < a.M;
+        const int64_t qc = in ? q : 0;
+        const int img = (int)(qc / HW), rem = (int)(qc - img * HW), y = rem / a.W;
+        qpix[u] = (int)qc;
+        qy[u] = in ? y : -(1 << 28);
+        const int64_t q1 = p0 + row;
+        const bool in1 = wid < kWinThird && row < kPT && q1 < a.M;
+        const int64_t qc1 = in1 ? q1 : 0;
+        const int img1 = (int)(qc1 / HW), rem1 = (int)(qc1 - img1 * HW), y1 = rem1 / a.W, x1 = rem1 - y1 * a.W;
+        qds[u] = a.mode2 == PV_CONV_X2_1X1 && in1
+                     ? (uint32_t)(((img1 * a.H2 + y1 * a.s2) * a.W2 + x1 * a.s2) * a.Cin2 * 2) + seg16
+                     : 0x80000000u;
+    }
+    const int wn = wid % WC, wm = wid / WC;
+    // x of this lane's B-operand pixel in each 16-pixel group (zero padding of shifted taps)
+    int xp[4];
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
         const int64_t p = p0 + wm * 64 + ni * 16 + (lane & 15);
-        const bool pv = p < a.M;
-        const int64_t pc = pv ? p : 0;
-        h4 r[MI];
-        if (a.res) {
+        const int64_t pc = p < a.M ? p : 0;
+        xp[ni] = (int)((pc % HW) % a.W);
+    }
+    // step s -> window j, its first step and length; 3x3 part: (cb s / 9, ky, kx)
+    auto win_of = [&](int s) { return s < a.nmain ? s / 3 : a.nmain / 3 + (s - a.nmain); };
+    auto win_first = [&](int j) { return j < a.nmain / 3 ? 3 * j : a.nmain + (j - a.nmain / 3); };
+    auto issue_w = [&](int s, int buf) {
+        // K index of step s: (cb, tap) -> tap * cbk + cb (the weights' memory order)
+        const int ks = s < a.nmain ? (s % 9) * cbk + s / 9 : s;
+        uint8_t *st = lds + buf * WST;
 #pragma unroll
-            for (int mi = 0; mi < MI; ++mi)
-                r[mi] = *(const h4 *)(a.res + pc * a.Cout + n0 + wn * (MI * 16) + mi * 16 + 4 * (lane >> 4));
+        for (int i = 0; i < NW; ++i) glds16(wr, st + (NW * wid + i) * 1024, woff[i], ks * RB);
+    };
+    // third u of window j (its piece u * kWinThird + wid) into window buffer j & 1
+    auto issue_third = [&](int j, int u) {
+        if (wid >= kWinThird) return;
+        const int piece = u * kWinThird + wid;
+        if (piece >= kWinPieces) return;
+        uint8_t *st = lds + 2 * WST + (j & 1) * XST + piece * 1024;
+        if (j >= a.nmain / 3) {                       // the downsample's 1x1 input, channel block j - nmain/3
+            const uint32_t cbo = (uint32_t)(j - a.nmain / 3) * RB;
+            glds16(x2r, st, qds[u] + cbo, 0);
+            return;
         }
+        const int cb = j / 3, ky = j - 3 * cb;
+        const int dy = (ky - 1) * d;
+        const bool second = a.mode2 == PV_CONV_X2_CAT && cb >= a.cb1;
+        const int C = second ? a.Cin2 : a.Cin;
+        const uint32_t cbo = (uint32_t)((second ? cb - a.cb1 : cb) * RB);
+        const bool ok = (unsigned)(qy[u] + dy) < (unsigned)a.H;
+        const uint32_t off = ok ? (uint32_t)((qpix[u] + dy * a.W) * C * 2) + cbo + seg16 : 0x80000000u;
+        glds16(second ? x2r : xr, st, off, 0);
+    };
+    f4v acc[MI][4];
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f4v{0.f, 0.f, 0.f, 0.f};
+    // kc-th half of step s (32 of its 64 channels): A from weight stage wst, B
+    // from window buffer xst at row shift sh, lanes outside their image row
+    // (mask bit ni clear) zeroed
+    auto compute_kc = [&](const uint8_t *wst, const uint8_t *xst, int sh, unsigned msk, int kc) {
+        const int sg = kc * 4 + (lane >> 4);
+        h8v af[MI], bf[4];
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi) {
-            const int c = n0 + wn * (MI * 16) + mi * 16 + 4 * (lane >> 4);
-            h4 y;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) y[j] = (_Float16)((float)(_Float16)acc[mi][ni][j] + (float)bq[mi][j]);
-            if (a.res) {
-                h4 rr = r[mi];
-                if (a.rbias) {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) rr[j] = (_Float16)((float)rr[j] + (float)rbq[mi][j]);
-                }
-#pragma unroll
-                for (int j = 0; j < 4; ++j) y[j] = (_Float16)((float)y[j] + (float)rr[j]);
-            } else if (a.rbias) {
-                // the downsample's bias (its convolution summed in the accumulator)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) y[j] = (_Float16)((float)y[j] + (float)rbq[mi][j]);
-            }
-            if (a.act == 1) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) y[j] = (float)y[j] > 0.f ? y[j] : (_Float16)0.f;
-            } else if (a.act == 2) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) y[j] = (float)y[j] > 0.f ? y[j] : (_Float16)((float)y[j] * a.slope);
-            }
-            if (pv) *(h4 *)(a.out + p * a.ldo + c) = y;
+            const int r = wn * (MI * 16) + mi * 16 + (lane & 15);
+            af[mi] = *(const h8v *)(wst + conv_granule(r, sg) * 16);
         }
+        const int r0 = wm * 64 + (lane & 15) + sh;
+        const uint8_t *b0 = xst + conv_granule(r0, sg) * 16;     // + ni * 16 rows keeps the swizzle
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            bf[ni] = *(const h8v *)(b0 + ni * 16 * RB);
+            if (!((msk >> ni) & 1)) bf[ni] = h8v{};
+        }
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+                acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mi], bf[ni], acc[mi][ni], 0, 0, 0);
+    };
+    const int ksteps = a.ksteps;
+    const int k0 = tail < 0 ? 0 : part * ksteps / a.nsplit;
+    const int k1 = tail < 0 ? ksteps : (part + 1) * ksteps / a.nsplit;
+    issue_w(k0, 0);
+    {
+        const int j0 = win_of(k0);
+        for (int u = 0; u < 3; ++u) issue_third(j0, u);
     }
+    for (int s = k0; s < k1; ++s) {
+        const int wbuf = (s - k0) & 1;
+        const int j = win_of(s), f = win_first(j), len = j < a.nmain / 3 ? 3 : 1, t = s - f;
+        __builtin_amdgcn_s_waitcnt(0x0F70);          // this wave's loads for step s have landed (vmcnt 0)
+        __syncthreads();                              // ... and every wave's; step s-1's reads are done
+        // B rows of this step: window row = tile row + d + dx (3x3) or the tile row (1x1)
+        int sh = 0;
+        unsigned msk = 0xF;
+        if (j < a.nmain / 3) {
+            const int dx = (t - 1) * d;               // kx = t
+            sh = d + dx;
+            if (dx != 0) {
+                msk = 0;
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni) msk |= ((unsigned)(xp[ni] + dx) < (unsigned)a.W ? 1u : 0u) << ni;
+            }
+        }
+        const uint8_t *wst = lds + wbuf * WST, *xst = lds + 2 * WST + (j & 1) * XST;
+        compute_kc(wst, xst, sh, msk, 0);
+        if (s + 1 < k1) issue_w(s + 1, wbuf ^ 1);
+        // the next window's thirds: this step's own, plus the earlier ones when
+        // the part started inside window j, plus the rest at the window's last step
+        if (win_first(j + 1) < k1) {
+            const int lo = s == k0 ? 0 : t, hi = t == len - 1 ? 2 : t;
+            for (int u = lo; u <= hi; ++u) issue_third(j + 1, u);
+        }
+        compute_kc(wst, xst, sh, msk, 1);
+    }
+    conv_finish<CT, MI, WC>(a, acc, tail, part, n0, p0, wn, wm, lane, lds);
 }
+#endif  // PVC_WINDOW
 
 
 // ==========================================================================
@@ -1402,8 +1623,16 @@ extern "C" int pv_conv3x3_ex_f16(const void *x, int32_t hin, int32_t win, int32_
         }
     }
     const unsigned grid = (unsigned)(a.nfull + (a.ntiles - a.nfull) * a.nsplit);
-    if (wide) k_conv3x3<kCT><<<grid, 64 * kNW, 0, (hipStream_t)stream>>>(a);
-    else k_conv3x3<128><<<grid, 64 * kNW, 0, (hipStream_t)stream>>>(a);
+#if PVC_WINDOW
+    if (stride == 1 && dil <= kMaxDil) {
+        if (wide) k_conv3x3w<kCT><<<grid, 64 * kNW, 0, (hipStream_t)stream>>>(a);
+        else k_conv3x3w<128><<<grid, 64 * kNW, 0, (hipStream_t)stream>>>(a);
+    } else
+#endif
+    {
+        if (wide) k_conv3x3<kCT><<<grid, 64 * kNW, 0, (hipStream_t)stream>>>(a);
+        else k_conv3x3<128><<<grid, 64 * kNW, 0, (hipStream_t)stream>>>(a);
+    }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? PV_OK : (int)e;
 }

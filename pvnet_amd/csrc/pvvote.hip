@@ -1263,14 +1263,23 @@ typedef _Float16 h4f __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kMB = 16;                        // pixels per MFMA batch (32 rows: 16 pixels x (X, Y))
-constexpr int kMChunk = 384;                   // pixels per sub-chunk: a unit's range (~350 px at configs[1]) in one
+#ifndef PVM_CHUNK
+#define PVM_CHUNK 352
+#endif
+#ifndef PVM_QUEUE
+#define PVM_QUEUE 128
+#endif
+// pixels per sub-chunk: a unit's range (~350 px at configs[1]) in one; 352
+// (with a 128-entry band queue) keeps the block's LDS under 40 KiB, so a
+// fourth block -- the next image's -- fits beside a launch's three per CU
+constexpr int kMChunk = PVM_CHUNK;
 constexpr int kMSlots = (kMChunk + 255) / 256; // pixels per thread in the block's staging (2)
 constexpr int kMBatch = kMChunk / kMB;         // batches per sub-chunk (24)
 static_assert(kMChunk % kMB == 0 && kMBatch <= 32 && kMChunk <= 512, "hit masks: 2 x 64 bits; queue: 9-bit pixel");
 constexpr int kMSet = 4;                       // 32-hypothesis column sets per wave (128 hypotheses)
 constexpr float kMHypMax = 8.0e6f;             // |hx|, |hy| above -> exact-only (keeps s >= 2^-9)
 constexpr float kMRMax = 30000.f;              // sub-chunk radius above -> exact sub-chunk (fp16 range of b)
-constexpr int kMQueue = 256;                   // band pairs queued per wave before a reference pass
+constexpr int kMQueue = PVM_QUEUE;             // band pairs queued per wave before a reference pass
 
 template <bool PREPPED>
 struct MSlab {
@@ -1365,12 +1374,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
             hlds[i * kWave + lane] = hv;
         }
         __builtin_amdgcn_wave_barrier();
-        float2 hev[kMSet];
+        // (the exact hypotheses stay in LDS, hlds[set * 32 + col]: read where
+        // needed rather than held in registers across the hot loop)
 #pragma unroll
         for (int j = 0; j < kMSet; ++j) {
             const int h = hg * kGroup + j * 32 + col;
             const float2 hv = hlds[j * 32 + col];
-            hev[j] = hv;
             const bool fin = isfinite(hv.x) && isfinite(hv.y);
             const bool xo = h < a.nh && fin &&
                             (hyp_exact_only(hv.x, hv.y) || !(fabsf(hv.x) < kMHypMax && fabsf(hv.y) < kMHypMax));
@@ -1477,16 +1486,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
             __syncthreads();
             if (!slow) {
                 // ---- the hypotheses' B fragments and bands for this origin ----
-                h4f bf[kMSet];
-                float gb[kMSet], sc[kMSet], Bh[kMSet];
-#pragma unroll
-                for (int j = 0; j < kMSet; ++j) {
+                // hypothesis j's scale s = 2^-k (|h' s| < 2^14) and bound B >=
+                // |h'| + |c'| + 1 (the +1 covers the fp16 subnormal terms) for
+                // this origin; made again for the band pairs (not held across
+                // the hot loop)
+                auto hscale = [&](int j, float &hx, float &hy, float &s, float &Bv) {
                     const bool fj = (hfm >> j) & 1u;
-                    const float hx = hev[j].x - ox, hy = hev[j].y - oy;
+                    const float2 hv = hlds[j * 32 + col];
+                    hx = hv.x - ox;
+                    hy = hv.y - oy;
                     const float mag = fmaxf(fabsf(hx), fabsf(hy));
                     const int e = __builtin_amdgcn_frexp_expf(mag);       // mag < 2^e
                     const int k = fj ? max(0, e - 14) : 0;
-                    const float s = __builtin_ldexpf(1.f, -k);
+                    s = __builtin_ldexpf(1.f, -k);
+                    Bv = (__builtin_amdgcn_sqrtf(fmaf(hx, hx, hy * hy)) * 1.00001f + R) * 1.00001f + 1.f;
+                };
+                h4f bf[kMSet];
+                float gb[kMSet];
+#pragma unroll
+                for (int j = 0; j < kMSet; ++j) {
+                    const bool fj = (hfm >> j) & 1u;
+                    float hx, hy, s, Bv;
+                    hscale(j, hx, hy, s, Bv);
                     const float hxs = hx * s, hys = hy * s;               // exact
                     const _Float16 xh_ = (_Float16)hxs, xl_ = (_Float16)(hxs - (float)xh_);
                     const _Float16 yh_ = (_Float16)hys, yl_ = (_Float16)(hys - (float)yh_);
@@ -1494,10 +1515,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                     h4f f = half ? h4f{yl_, yh_, sh, sh} : h4f{xh_, xl_, xh_, yh_};
                     if (!fj) f = h4f{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
                     bf[j] = f;
-                    // B >= |h'| + |c'| + 1 (the +1 covers the fp16 subnormal terms)
-                    const float Bv = (__builtin_amdgcn_sqrtf(fmaf(hx, hx, hy * hy)) * 1.00001f + R) * 1.00001f + 1.f;
-                    Bh[j] = Bv;
-                    sc[j] = s;
                     gb[j] = fj ? (a.gzf + a.gzr) * Bv * s * 1.00001f : -1.f;
                 }
                 uint32_t neg[kMSet] = {0u, 0u, 0u, 0u};
@@ -1599,10 +1616,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                     const int p = bit / kMSet, j = bit % kMSet;
                     ++nfix;
                     h4f bj = bf[0];
-                    float gBj = Bh[0], sj = sc[0];
 #pragma unroll
                     for (int k = 1; k < kMSet; ++k)
-                        if (j == k) { bj = bf[k]; gBj = Bh[k]; sj = sc[k]; }
+                        if (j == k) bj = bf[k];
+                    float hxj, hyj, sj, gBj;
+                    hscale(j, hxj, hyj, sj, gBj);
                     const bool fj = (hfm >> j) & 1u;
                     const float G = a.gzf * gBj * sj * 1.001f;
                     const f32x16 c = __builtin_amdgcn_mfma_f32_32x32x8f16(afrag(p), bj, zero, 0, 0, 0);
@@ -1655,7 +1673,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                         const float2 hx2 = hlds[j * 32 + l];
                         int c = 0;
 #pragma unroll
-                        for (int k = 0; k < kMChunk / kWave; ++k) {
+                        for (int k = 0; k < (kMChunk + kWave - 1) / kWave; ++k) {
                             const int jj = k * kWave + lane;
                             bool e = false;
                             if (jj < np) {
@@ -1676,7 +1694,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                     const F4 e = S.x.get(jj);
 #pragma unroll
                     for (int j = 0; j < kMSet; ++j)
-                        if ((hfm | hxm) >> j & 1u) cnt[j] += exact_vote(e.z, e.w, e.x, e.y, hev[j].x, hev[j].y, a.thr);
+                        if ((hfm | hxm) >> j & 1u) {
+                            const float2 hv = hlds[j * 32 + col];
+                            cnt[j] += exact_vote(e.z, e.w, e.x, e.y, hv.x, hv.y, a.thr);
+                        }
                 }
             }
         }
@@ -3270,7 +3291,7 @@ const char *pv_version(void) { return PV_VERSION; }
 #define PVV_STR2(x) #x
 #define PVV_STR(x) PVV_STR2(x)
 const char *pv_build_config(void) {
-    return "vote=k_vote_mfma(bpc=" PVV_STR(PVV_VM_BPC) ",wpe=" PVM_WPE_STR ",chunk=384,rw=" PVV_STR(PVV_VM_RW3_0) "/"
+    return "vote=k_vote_mfma(bpc=" PVV_STR(PVV_VM_BPC) ",wpe=" PVM_WPE_STR ",chunk=" PVV_STR(PVM_CHUNK) ",queue=" PVV_STR(PVM_QUEUE) ",rw=" PVV_STR(PVV_VM_RW3_0) "/"
            PVV_STR(PVV_VM_RW3_1) "/" PVV_STR(PVV_VM_RW3_2) ")"
            " hypgen=" PVV_STR(PVV_HYPGEN)
            " refine=" PVV_STR(PVV_REFINE_NJ) "x" PVV_STR(PVV_REFINE_T)

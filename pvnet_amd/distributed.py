@@ -20,7 +20,7 @@ from typing import Callable, Optional, Sequence
 import torch
 import torch.distributed as dist
 
-__all__ = ["shard", "gather_results", "run_stream"]
+__all__ = ["shard", "gather_results", "gather_results_multi", "run_stream"]
 
 
 def shard(n_images: int, rank: int, world: int) -> list[int]:
@@ -61,9 +61,30 @@ def gather_results(local: torch.Tensor, n_images: int, rank: int, world: int,
     return out.to(local.device) if stage else out
 
 
+def gather_results_multi(parts: Sequence[torch.Tensor], n_images: int, rank: int, world: int,
+                         group: Optional[dist.ProcessGroup] = None) -> tuple:
+    """:func:`gather_results` for a result of several tensors per image (the
+    configs[4] stream: keypoints [vn, 2] f32, covariances [vn, 2, 2] f32,
+    pose [3, 4] f64).  Each part is ``[len(shard), *shape_k]``; they travel
+    as one f64 row per image (every f32 is exact in f64), so one collective
+    moves them all.  Returns a tuple of ``[n_images, *shape_k]`` in stream
+    order, each in its part's dtype."""
+    n = int(parts[0].shape[0])
+    if any(int(p.shape[0]) != n for p in parts):
+        raise ValueError("every part needs one row per image of the shard")
+    sizes = [int(torch.Size(p.shape[1:]).numel()) for p in parts]
+    flat = torch.cat([p.reshape(n, k).to(torch.float64) for p, k in zip(parts, sizes)], 1)
+    allf = gather_results(flat, n_images, rank, world, group)
+    out, o = [], 0
+    for p, k in zip(parts, sizes):
+        out.append(allf[:, o:o + k].reshape((n_images,) + tuple(p.shape[1:])).to(p.dtype))
+        o += k
+    return tuple(out)
+
+
 def run_stream(load: Callable[[int], Sequence[torch.Tensor]], vote: Callable[..., torch.Tensor], n_images: int,
-               rank: int, world: int, result_shape: Sequence[int], device: torch.device,
-               dtype: torch.dtype = torch.float32, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+               rank: int, world: int, result_shape, device: torch.device,
+               dtype=torch.float32, group: Optional[dist.ProcessGroup] = None):
     """Vote every image of this rank's shard, then gather all results.
 
     ``load(i)`` returns the arguments of ``vote`` for image i (already on
@@ -71,9 +92,26 @@ def run_stream(load: Callable[[int], Sequence[torch.Tensor]], vote: Callable[...
     ``result_shape`` (e.g. ``ransac_voting_layer_v3_from_network`` ->
     ``[1, vn, 2]`` with result_shape ``(vn, 2)``).  Returns
     ``[n_images, *result_shape]`` in stream order on every rank.
+
+    A result of several tensors (e.g. keypoints, covariances and the pose of
+    configs[4]): ``vote`` returns a tuple, ``result_shape`` is a list of
+    shapes and ``dtype`` a list of dtypes; the return value is then a tuple
+    (:func:`gather_results_multi`).
     """
     mine = shard(n_images, rank, world)
-    local = torch.empty((len(mine),) + tuple(result_shape), dtype=dtype, device=device)
+    multi = len(result_shape) > 0 and isinstance(result_shape[0], (tuple, list, torch.Size))
+    if not multi:
+        local = torch.empty((len(mine),) + tuple(result_shape), dtype=dtype, device=device)
+        for k, i in enumerate(mine):
+            local[k] = vote(*load(i)).reshape(tuple(result_shape))
+        return gather_results(local, n_images, rank, world, group)
+    dtypes = list(dtype) if isinstance(dtype, (tuple, list)) else [dtype] * len(result_shape)
+    locals_ = [torch.empty((len(mine),) + tuple(sh), dtype=dt, device=device)
+               for sh, dt in zip(result_shape, dtypes)]
     for k, i in enumerate(mine):
-        local[k] = vote(*load(i)).reshape(tuple(result_shape))
-    return gather_results(local, n_images, rank, world, group)
+        res = vote(*load(i))
+        if len(res) != len(locals_):
+            raise ValueError(f"vote returned {len(res)} tensors, result_shape names {len(locals_)}")
+        for loc, r, sh in zip(locals_, res, result_shape):
+            loc[k] = r.reshape(tuple(sh))
+    return gather_results_multi(locals_, n_images, rank, world, group)

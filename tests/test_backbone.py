@@ -26,6 +26,7 @@ import torch
 
 from pvnet_amd.network import PVNet, PVNetInference, fold_batchnorm, upsample2x_cat
 from tests import backbone_init as BI
+from tests import fp16_bounds as B
 from tests.golden_io import load
 
 G = load("backbone_g4")
@@ -344,7 +345,9 @@ def test_segmentation_mask_device_fp16(vd, device):
           f"{2 * FP16_TOL * sc:.3f}); vertex direction vs fp32: median {np.median(ang):.2e}, "
           f"p99 {np.quantile(ang, 0.99):.2e}, max {ang.max():.2e} rad")
     assert np.all(np.abs(d_own[diff]) <= 2 * FP16_TOL * sc)
-    assert diff.size <= 0.05 * d_own.size
+    # measured 0.8 % (PVnet(18, 2)) and 2.4 % (PVnet(42, 2)) of the frame
+    # (DESIGN.md 3); the gate is that count plus a quarter
+    assert diff.size <= {18: 0.012, 42: 0.03}[vd] * d_own.size
 
 
 @pytest.mark.gpu
@@ -465,6 +468,7 @@ def test_decoder_tail_matches_torch(cout, hw, device):
           f"mean {float(d.mean()):.3e} (tolerance {tol:.3e}, scale {sc:.2f})")
     assert float(d.max()) <= tol
     assert float(d.mean()) <= 2 ** -12 * sc
+    _check_decoder_fp64(got, fm, img, c0, 0.1, f"decoder tail cout {cout}", head=(c1.weight, c1.bias))
 
 
 @pytest.mark.gpu
@@ -548,6 +552,25 @@ def test_conv3x3_matches_torch(case, device):
     print(f"conv3x3 {case}: max dev {float(dev_.max()):.3e}, mean {float(dev_.mean()):.2e} (scale {sc:.2f})")
     assert float(dev_.max()) <= 2 ** -8 * sc
     assert float(dev_.mean()) <= 2 ** -13 * sc
+    # against an f64 convolution of the same fp16 inputs: only the f32
+    # accumulation and the epilogue's fp16 roundings (tests/fp16_bounds.py)
+    with torch.no_grad():
+        c64 = B.conv64(x, conv.weight, padding=d, dilation=d)
+        e = B.round_step(c64, B.acc_bound(x, conv.weight, 9 * cin, padding=d, dilation=d))   # fp16 conv output
+        y64 = c64 + conv.bias.double().view(1, -1, 1, 1)
+        e = B.round_step(y64, e)                                                               # + bias
+        if use_res:
+            r64 = res.double() + (rb.double().view(1, -1, 1, 1) if use_rb else 0.0)
+            if use_rb:
+                e = e + B.hulp(r64)                                                            # res + rbias
+            y64 = y64 + r64
+            e = B.round_step(y64, e)                                                           # + residual
+        if act == "leaky":
+            e = B.leaky_step(y64, e, 0.1)
+            y64 = F.leaky_relu(y64, 0.1)
+        else:
+            y64 = torch.relu(y64)
+    B.check(got, y64, e, f"conv3x3 {case}")
 
 
 @pytest.mark.gpu
@@ -618,6 +641,32 @@ def test_conv3x3_ex_matches_torch(case, device):
     print(f"conv3x3_ex {case}: max dev {float(dev_.max()):.3e}, mean {float(dev_.mean()):.2e} (scale {sc:.2f})")
     assert float(dev_.max()) <= 2 ** -8 * sc
     assert float(dev_.mean()) <= 2 ** -13 * sc
+    # against an f64 convolution of the same fp16 inputs (tests/fp16_bounds.py):
+    # the 1x1 downsample is summed in the same accumulator, rounded once
+    with torch.no_grad():
+        if kind == "s2":
+            c64 = B.conv64(x, wt, stride=2, padding=d, dilation=d)
+            e = B.acc_bound(x, wt, 9 * cin, stride=2, padding=d, dilation=d)
+        elif kind == "cat":
+            xc = torch.cat([x, x2], 1)
+            c64 = B.conv64(xc, wt, padding=d, dilation=d)
+            e = B.acc_bound(xc, wt, 9 * (cin + c2), padding=d, dilation=d)
+        else:
+            c64 = B.conv64(y, wt, padding=d, dilation=d) + B.conv64(xin, wd, stride=s2)
+            e = B.acc_bound(y, wt, 9 * cmid + cin, padding=d, dilation=d) + \
+                B.acc_bound(xin, wd, 9 * cmid + cin, stride=s2)
+        e = B.round_step(c64, e)
+        y64 = c64 + b.double().view(1, -1, 1, 1)
+        e = B.round_step(y64, e)
+        if kind.startswith("ds"):
+            y64 = y64 + bd.double().view(1, -1, 1, 1)
+            e = B.round_step(y64, e)
+        if kind == "cat":
+            e = B.leaky_step(y64, e, 0.1)
+            y64 = F.leaky_relu(y64, 0.1)
+        else:
+            y64 = torch.relu(y64)
+    B.check(got, y64, e, f"conv3x3_ex {case}")
 
 
 def test_conv3x3_weight_with_downsample():
@@ -666,6 +715,7 @@ def test_decoder_conv2s_matches_torch(hw, device):
     print(f"decoder conv2s {2 * h}x{2 * w}: max dev {float(d.max()):.3e}, mean {float(d.mean()):.2e} (scale {sc:.2f})")
     assert float(d.max()) <= 2 ** -7 * sc
     assert float(d.mean()) <= 2 ** -12 * sc
+    _check_decoder_fp64(got, fm, skip, c, 0.1, "decoder conv2s")
 
 
 def test_decoder_conv_weight_layouts():
@@ -721,6 +771,37 @@ def test_decoder_conv4s_matches_torch(hw, device):
     print(f"decoder conv4s {2 * h}x{2 * w}: max dev {float(d.max()):.3e}, mean {float(d.mean()):.2e} (scale {sc:.2f})")
     assert float(d.max()) <= 2 ** -7 * sc
     assert float(d.mean()) <= 2 ** -12 * sc
+    _check_decoder_fp64(got, fm, skip, c, 0.1, "decoder conv4s")
+
+
+def _check_decoder_fp64(got, fm, skip, c, slope, name, head=None):
+    """A decoder kernel against the f64 reference of the same fp16 inputs:
+    upsample x2 (align_corners) + cat + 3x3 conv + bias + LeakyReLU (+ the 1x1
+    head conv + bias), bounded by the fp16 blend (BLEND x the blended sources'
+    largest |fm|, through sum |w|), the f32 accumulation and each fp16
+    rounding of the epilogue (tests/fp16_bounds.py)."""
+    F = torch.nn.functional
+    with torch.no_grad():
+        up = F.interpolate(fm.double(), scale_factor=2, mode="bilinear", align_corners=True)
+        xin = torch.cat([up, skip.double()], 1)
+        cin = xin.shape[1]
+        c64 = B.conv64(xin, c.weight, padding=1)
+        eb = torch.cat([B.BLEND * B.blend_source_max(fm), torch.zeros_like(skip, dtype=torch.float64)], 1)
+        e = B.conv64(eb, c.weight.abs(), padding=1) + B.acc_bound(xin, c.weight, 9 * cin, padding=1)
+        e = B.round_step(c64, e)                                    # the conv's fp16 output
+        y64 = c64 + c.bias.double().view(1, -1, 1, 1)
+        e = B.round_step(y64, e)                                    # + bias (fp16 add)
+        e = B.leaky_step(y64, e, slope)
+        y64 = F.leaky_relu(y64, slope)
+        if head is not None:                                        # the tail's 1x1 conv + bias
+            w2, b2 = head
+            k = w2.shape[1]
+            e = B.conv64(e, w2.abs()) + B.acc_bound(y64, w2, k)
+            y64 = B.conv64(y64, w2)
+            e = B.round_step(y64, e)
+            y64 = y64 + b2.double().view(1, -1, 1, 1)
+            e = B.round_step(y64, e)
+    B.check(got, y64, e, name)
 
 
 def test_stem_weight_layout():
@@ -780,6 +861,12 @@ def test_stem_conv_matches_torch(hw, device):
     print(f"stem conv {h}x{w}: max dev {float(d.max()):.3e}, mean {float(d.mean()):.2e} (scale {sc:.2f})")
     assert float(d.max()) <= 2 ** -7 * sc
     assert float(d.mean()) <= 2 ** -12 * sc
+    with torch.no_grad():                     # against an f64 convolution of the same inputs (tests/fp16_bounds.py)
+        c64 = B.conv64(img, c.weight, stride=2, padding=3)
+        e = B.round_step(c64, B.acc_bound(img, c.weight, 3 * 49, stride=2, padding=3))
+        y64 = c64 + c.bias.double().view(1, -1, 1, 1)
+        e = B.round_step(y64, e)
+    B.check(got, torch.relu(y64), e, f"stem conv {h}x{w}")
     assert pool.is_contiguous(memory_format=cl) and torch.equal(pool, F.max_pool2d(got, 3, 2, 1))
 
 
@@ -831,6 +918,17 @@ def test_conv64_matches_torch(case, device):
     print(f"conv64 {case}: max dev {float(d.max()):.3e}, mean {float(d.mean()):.2e} (scale {sc:.2f})")
     assert float(d.max()) <= 2 ** -8 * sc
     assert float(d.mean()) <= 2 ** -13 * sc
+    with torch.no_grad():                     # against an f64 convolution of the same inputs (tests/fp16_bounds.py)
+        c64 = B.conv64(x, c.weight, padding=1)
+        e = B.round_step(c64, B.acc_bound(x, c.weight, 9 * 64, padding=1))
+        y64 = c64 + c.bias.double().view(1, -1, 1, 1)
+        e = B.round_step(y64, e)
+        if kind == "res":
+            y64 = y64 + res.double()
+            e = B.round_step(y64, e)
+        if kind != "none":
+            y64 = torch.relu(y64)
+    B.check(got, y64, e, f"conv64 {case}")
 
 def test_conv3x3_ex_eligibility():
     """Which convolutions PVNetInference routes to pv_conv3x3_ex_f16 (CPU):

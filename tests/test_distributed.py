@@ -64,3 +64,40 @@ def test_stream_gloo(tmp_path, world, n_images):
     got = np.load(out)
     want = np.stack([_oracle_vote(*_field(i)).numpy().reshape(3, 2) for i in range(n_images)])
     np.testing.assert_array_equal(got, want)
+
+
+def _multi_result(i):
+    """Image i's three-part result: keypoints f32 [3, 2], covariances f32
+    [3, 2, 2], pose f64 [3, 4] (values that f32 -> f64 -> f32 must keep)."""
+    g = torch.Generator().manual_seed(1000 + i)
+    return (torch.randn(3, 2, generator=g) * 100, torch.randn(3, 2, 2, generator=g),
+            torch.randn(3, 4, generator=g, dtype=torch.float64) / 3)
+
+
+def _multi_worker(rank, world, port, n_images, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = D.run_stream(lambda i: (i,), _multi_result, n_images, rank, world,
+                           [(3, 2), (3, 2, 2), (3, 4)], torch.device("cpu"),
+                           dtype=[torch.float32, torch.float32, torch.float64])
+        if rank == 0:
+            np.savez(out_path, *[r.numpy() for r in res])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world, n_images", [(2, 5), (3, 7), (2, 1)])
+def test_stream_multi_result_gloo(tmp_path, world, n_images):
+    """configs[4]'s stream result (keypoints, covariances, pose) gathered in
+    one collective: every part comes back in stream order, dtypes and values
+    unchanged."""
+    out = str(tmp_path / "multi.npz")
+    mp.spawn(_multi_worker, args=(world, _free_port(), n_images, out), nprocs=world, join=True)
+    got = np.load(out)
+    parts = [got[f"arr_{k}"] for k in range(3)]
+    for i in range(n_images):
+        want = _multi_result(i)
+        for p, w in zip(parts, want):
+            assert p.dtype == w.numpy().dtype
+            np.testing.assert_array_equal(p[i], w.numpy())

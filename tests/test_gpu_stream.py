@@ -158,3 +158,136 @@ def test_config3_stream_two_ranks_gloo(device, tmp_path):
     r0, r1 = np.load(out + ".0.npy"), np.load(out + ".1.npy")
     np.testing.assert_array_equal(r0, r1)
     check_against_oracle(r0, None)
+
+
+# ---------------------------------------------------------------- configs[4]: keypoints + covariances + poses
+# The YCB-Video stream (BASELINE.json configs[4]): per image ransac_voting_layer_v3
+# (hn 512) from the network layout, estimate_voting_distribution_with_mean
+# (16 x 256 hypotheses, RV:333-406) on argmax(seg) and the strided vertex view,
+# and the uncertainty PnP of the 21 keypoints (evaluation_utils.py:161-190);
+# the stream is sharded round-robin and (keypoints [21, 2], covariances
+# [21, 2, 2], pose [3, 4]) come back in one gather (the [vn, 2, 2] payload of
+# SURVEY 8(e)).  Even images are the golden ycb21 frame (the reference's own
+# keypoints and covariances, its idxs injected); odd ones are 21-keypoint
+# fields projected from random poses through the YCB camera (checked against
+# the oracle's v3 -> EVD -> PnP with the same injected idxs).
+N4 = 4
+COV4_RTOL = 1e-4
+
+
+def ycb_stream_inputs(i):
+    from tests import golden_io as G
+    g = G.load("ycb21_cases")
+    K, p3 = g["camera"], g["points_3d"]
+    if i % 2 == 0:
+        _, _, f = G.ycb_inputs(g)
+        i3 = g["v3_idxs"].astype(np.int32)
+        i4 = g["evdm_idxs"].astype(np.int32).reshape(1, -1, 21, 2)
+        return f, i3, i4, g
+    rng = np.random.default_rng(70_000 + i)
+    a = rng.normal(size=3) * 0.5
+    th = np.linalg.norm(a)
+    kx = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]]) / th
+    R = np.eye(3) + np.sin(th) * kx + (1 - np.cos(th)) * kx @ kx
+    X = p3 @ R.T + np.array([rng.uniform(-0.05, 0.05), rng.uniform(-0.05, 0.05), rng.uniform(0.9, 1.1)])
+    kp = np.stack([K[0, 0] * X[:, 0] / X[:, 2] + K[0, 2], K[1, 1] * X[:, 1] / X[:, 2] + K[1, 2]], 1)
+    f = synth.synthetic_field(7000 + i, vn=21, keypoints=kp, radius=40.0,
+                              center=(float(kp[:, 0].mean()), float(kp[:, 1].mean())))
+    tn = int(f["tn"])
+    i3 = rng.integers(0, tn, (1, HN, 21, 2)).astype(np.int32)
+    i4 = rng.integers(0, tn, (1, 16 * 256, 21, 2)).astype(np.int32)
+    return f, i3, i4, None
+
+
+def ycb_expected(i):
+    """(keypoints, covariances, pose) the stream must return for image i."""
+    from oracle import pnp as P
+    f, i3, i4, g = ycb_stream_inputs(i)
+    from tests import golden_io as G
+    gg = G.load("ycb21_cases")
+    K, p3 = gg["camera"], gg["points_3d"]
+    if g is not None:
+        kp, cov = g["v3_keypoints"][0], g["evdm_cov"][0]
+    else:
+        mask = np.argmax(f["seg"], 1)
+        vv = np.ascontiguousarray(f["vertex"].transpose(0, 2, 3, 1).reshape(1, 480, 640, 21, 2))
+        kp = O.ransac_voting_layer_v3(mask, vv, HN, idxs=[i3[0]])
+        _, cov = O.estimate_voting_distribution_with_mean(mask, vv, kp, idxs=[list(i4[0].reshape(16, 256, 21, 2))])
+        kp, cov = kp[0], cov[0]
+    return kp, cov, P.uncertainty_pnp(kp, P.weights_from_cov(cov), p3, K)
+
+
+def make_vote4(dev):
+    from pvnet_amd import extend_utils as eu
+    from pvnet_amd import ransac_voting_gpu as rvg
+    from tests import golden_io as G
+    gg = G.load("ycb21_cases")
+    K, p3 = gg["camera"], gg["points_3d"]
+    w1, w2 = rvg.VotingWorkspace(), rvg.VotingWorkspace()
+
+    def load(i):
+        f, i3, i4, _ = ycb_stream_inputs(i)
+        return (torch.from_numpy(f["seg"]).to(dev), torch.from_numpy(f["vertex"]).to(dev),
+                torch.from_numpy(i3).to(dev), torch.from_numpy(i4).to(dev))
+
+    def vote(seg, ver, i3, i4):
+        b, c, h, w = ver.shape
+        kp = rvg.ransac_voting_layer_v3_from_network(seg, ver, HN, _idxs=i3, _workspace=w1)
+        mask = seg.argmax(1)
+        vertex = ver.permute(0, 2, 3, 1).view(b, h, w, c // 2, 2)
+        mean, cov = rvg.estimate_voting_distribution_with_mean(mask, vertex, kp, _idxs=i4, _workspace=w2)
+        Rt = eu.pose_from_voting(mean, cov, p3, K)
+        return kp[0], cov[0], Rt[0]
+    return load, vote
+
+
+def check_ycb_stream(res):
+    kps, covs, poses = (r.cpu().numpy() for r in res)
+    assert kps.shape == (N4, 21, 2) and covs.shape == (N4, 21, 2, 2) and poses.shape == (N4, 3, 4)
+    assert poses.dtype == np.float64
+    for i in range(N4):
+        kp, cov, pose = ycb_expected(i)
+        np.testing.assert_allclose(kps[i], kp, atol=KP_TOL, rtol=0, err_msg=f"image {i}")
+        np.testing.assert_allclose(covs[i], cov, rtol=COV4_RTOL, atol=1e-4 * np.abs(cov).max(), err_msg=f"image {i}")
+        np.testing.assert_allclose(poses[i], pose, atol=1e-4, err_msg=f"image {i}")
+
+
+@pytest.mark.gpu
+def test_config4_stream_one_rank(device):
+    """configs[4] on one rank: keypoints, covariances and poses of every image."""
+    load, vote = make_vote4(device)
+    res = D.run_stream(load, vote, N4, 0, 1, [(21, 2), (21, 2, 2), (3, 4)], device,
+                       dtype=[torch.float32, torch.float32, torch.float64])
+    check_ycb_stream(res)
+
+
+def _rank_worker4(rank, world, port, out_path):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        load, vote = make_vote4(dev)
+        res = D.run_stream(load, vote, N4, rank, world, [(21, 2), (21, 2, 2), (3, 4)], dev,
+                           dtype=[torch.float32, torch.float32, torch.float64])
+        assert all(r.device == dev for r in res)
+        np.savez(out_path + f".{rank}.npz", *[r.cpu().numpy() for r in res])
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_config4_stream_two_ranks_gloo(device, tmp_path):
+    """configs[4] sharded over two ranks (both on cuda:0, gloo): each rank
+    votes, estimates the covariances and solves the poses of its round-robin
+    shard; one gather gives every rank the whole stream's keypoints,
+    covariances and poses in order, equal to the reference's / the oracle's."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "res4")
+    mp.spawn(_rank_worker4, args=(2, _free_port(), out), nprocs=2, join=True)
+    r0, r1 = np.load(out + ".0.npz"), np.load(out + ".1.npz")
+    for k in r0.files:
+        np.testing.assert_array_equal(r0[k], r1[k])
+    check_ycb_stream([torch.from_numpy(r0[f"arr_{k}"]) for k in range(3)])
