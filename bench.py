@@ -45,9 +45,9 @@ FP32_VECTOR_PEAK_TFLOPS = 157.3
 H, W, VN = 480, 640, 9
 
 
-PMC_FILE = "profiles/r03_pmc_traffic.json"
+PMC_FILE = "profiles/r04_pmc_traffic.json"
 U1_WARM, U1_TIMED = 5, 3            # measure_u1: graph replays (of 100 launches) untimed, then timed
-STATS_FILE = "profiles/r03_bench_kernel_stats.csv"
+STATS_FILE = "profiles/r04_bench_kernel_stats.csv"
 
 
 def pmc_traffic(kernel):
@@ -83,7 +83,8 @@ def parse():
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--skip-e2e", action="store_true")
     ap.add_argument("--skip-u1", action="store_true")
-    ap.add_argument("--skip-config3", action="store_true")
+    ap.add_argument("--skip-config3", action="store_true", help="skip the configs[3] and configs[4] stream legs")
+    ap.add_argument("--skip-u4", action="store_true", help="skip the U4 (EVD with mean) timing")
     ap.add_argument("--dry-run", action="store_true",
                     help="the multi-rank plumbing without a GPU (CPU tests): gloo ranks, each image's result is its "
                          "field's generating keypoints (no voting), then the timed region's barriers, the gather, "
@@ -1128,10 +1129,11 @@ def report(args, ws, res, final_err, dev):
                                          "traffic = 2*FETCH_SIZE + WRITE_SIZE per launch (%s)" % (STATS_FILE, PMC_FILE))
         except Exception as e:  # reported, never hides the main number
             line["roofline"] = {"error": repr(e)}
-    try:
-        line["roofline_evd"] = measure_u4(dev)
-    except Exception as e:  # reported, never hides the main number
-        line["roofline_evd"] = {"error": repr(e)}
+    if not args.skip_u4:
+        try:
+            line["roofline_evd"] = measure_u4(dev)
+        except Exception as e:  # reported, never hides the main number
+            line["roofline_evd"] = {"error": repr(e)}
     if not args.skip_e2e:
         for key, fn in (("e2e_config1", lambda: measure_e2e(dev)),
                         ("e2e_config2_fp16_batch32", lambda: measure_e2e(dev, half=True, batch=32)),

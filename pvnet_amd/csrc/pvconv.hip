@@ -794,7 +794,9 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3w(ConvArgs a) {
     constexpr int WC = kNW / 4;
     constexpr int MI = CT / WC / 16;
     static_assert(kWinThird <= kNW, "one window piece per wave and step");
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WST + 2 * XST];
+    // + a 128-byte zero block: the B rows of lanes whose shifted tap leaves its image row
+    __shared__ __attribute__((aligned(128))) uint8_t lds[2 * WST + 2 * XST + 128];
+    if (threadIdx.x < 8) *(uint4 *)(lds + 2 * WST + 2 * XST + 16 * threadIdx.x) = make_uint4(0u, 0u, 0u, 0u);
     const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
     int bid = (int)blockIdx.x, part = 0, tail = -1;
     if (bid < a.nfull) {
@@ -898,9 +900,10 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3w(ConvArgs a) {
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f4v{0.f, 0.f, 0.f, 0.f};
     // kc-th half of step s (32 of its 64 channels): A from weight stage wst, B
-    // from window buffer xst at row shift sh, lanes outside their image row
-    // (mask bit ni clear) zeroed
-    auto compute_kc = [&](const uint8_t *wst, const uint8_t *xst, int sh, unsigned msk, int kc) {
+    // from the LDS byte offsets boff[ni] of this step's kc 0 granules (kc 1's
+    // are boff ^ 64: segment 4 + q of a row lies at granule (4 + q) ^ (r & 7)
+    // = that of q, xor 4); a lane outside its image row points at the zero block
+    auto compute_kc = [&](const uint8_t *wst, const uint32_t (&boff)[4], int kc) {
         const int sg = kc * 4 + (lane >> 4);
         h8v af[MI], bf[4];
 #pragma unroll
@@ -908,18 +911,18 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3w(ConvArgs a) {
             const int r = wn * (MI * 16) + mi * 16 + (lane & 15);
             af[mi] = *(const h8v *)(wst + conv_granule(r, sg) * 16);
         }
-        const int r0 = wm * 64 + (lane & 15) + sh;
-        const uint8_t *b0 = xst + conv_granule(r0, sg) * 16;     // + ni * 16 rows keeps the swizzle
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-            bf[ni] = *(const h8v *)(b0 + ni * 16 * RB);
-            if (!((msk >> ni) & 1)) bf[ni] = h8v{};
-        }
+        for (int ni = 0; ni < 4; ++ni) bf[ni] = *(const h8v *)(lds + (boff[ni] ^ (uint32_t)(kc * 64)));
+#ifdef PVC_NO_MFMA
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) acc[mi][0][0] += (float)af[mi][0] + (float)bf[mi & 3][1];
+#else
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni)
                 acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mi], bf[ni], acc[mi][ni], 0, 0, 0);
+#endif
     };
     const int ksteps = a.ksteps;
     const int k0 = tail < 0 ? 0 : part * ksteps / a.nsplit;
@@ -946,8 +949,16 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3w(ConvArgs a) {
                 for (int ni = 0; ni < 4; ++ni) msk |= ((unsigned)(xp[ni] + dx) < (unsigned)a.W ? 1u : 0u) << ni;
             }
         }
-        const uint8_t *wst = lds + wbuf * WST, *xst = lds + 2 * WST + (j & 1) * XST;
-        compute_kc(wst, xst, sh, msk, 0);
+        const uint8_t *wst = lds + wbuf * WST;
+        uint32_t boff[4];
+        {
+            const int r0 = wm * 64 + (lane & 15) + sh;
+            const uint32_t b0 = (uint32_t)(2 * WST + (j & 1) * XST + conv_granule(r0, lane >> 4) * 16);
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)          // + ni * 16 rows keeps the swizzle
+                boff[ni] = (msk >> ni) & 1 ? b0 + (uint32_t)(ni * 16 * RB) : (uint32_t)(2 * WST + 2 * XST);
+        }
+        compute_kc(wst, boff, 0);
         if (s + 1 < k1) issue_w(s + 1, wbuf ^ 1);
         // the next window's thirds: this step's own, plus the earlier ones when
         // the part started inside window j, plus the rest at the window's last step
@@ -955,7 +966,7 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3w(ConvArgs a) {
             const int lo = s == k0 ? 0 : t, hi = t == len - 1 ? 2 : t;
             for (int u = lo; u <= hi; ++u) issue_third(j + 1, u);
         }
-        compute_kc(wst, xst, sh, msk, 1);
+        compute_kc(wst, boff, 1);
     }
     conv_finish<CT, MI, WC>(a, acc, tail, part, n0, p0, wn, wm, lane, lds);
 }

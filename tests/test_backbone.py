@@ -949,3 +949,47 @@ def test_conv3x3_ex_eligibility():
     assert len(dss) == 3 and all(downsample_eligible(d) for d in dss)
     assert not downsample_eligible(None)
     assert not downsample_eligible(nn.Sequential(nn.Conv2d(64, 128, 1, 2, bias=False)))
+
+
+@pytest.mark.gpu
+def test_conv_split_scratch_capture_without_warmup(device):
+    """The split-K scratch of pv_conv3x3_ex_f16 and graph capture (advisor,
+    round 3): capture a convolution whose last round of tiles is split, on a
+    fresh stream with no warm-up, then run the same call eagerly on that stream
+    BEFORE any replay, then replay.  The capture runs without split-K (no
+    buffer is made inside it), the eager calls make and zero a buffer outside
+    it; every output is within the fp16 bound of the f64 convolution, the two
+    eager calls are bit-equal, and the replay equals the captured form."""
+    from pvnet_amd.network import clear_conv_workspaces, conv3x3, conv3x3_weight
+    F = torch.nn.functional
+    g = torch.Generator().manual_seed(404)
+    cl = torch.channels_last
+    n, cin, cout, h, w, d = 16, 128, 128, 60, 80, 1
+    x = torch.randn(n, cin, h, w, generator=g).to(device, torch.float16).contiguous(memory_format=cl)
+    conv = torch.nn.Conv2d(cin, cout, 3, 1, d, d, bias=True).to(device)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5))
+        conv.bias.copy_(torch.randn(cout, generator=g) * 0.5)
+    conv = conv.half()
+    wt = conv3x3_weight(conv)
+    clear_conv_workspaces()
+    s = torch.cuda.Stream(device=device)
+    graph = torch.cuda.CUDAGraph()
+    with torch.no_grad(), torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            got_g = conv3x3(x, wt, conv.bias, d, "relu")
+        e1 = conv3x3(x, wt, conv.bias, d, "relu")          # eager, before any replay
+        e2 = conv3x3(x, wt, conv.bias, d, "relu")
+    s.synchronize()
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(e1, e2)
+    with torch.no_grad():
+        c64 = B.conv64(x, conv.weight, padding=d, dilation=d)
+        e = B.round_step(c64, B.acc_bound(x, conv.weight, 9 * cin, padding=d, dilation=d))
+        y64 = c64 + conv.bias.double().view(1, -1, 1, 1)
+        e = B.round_step(y64, e)
+        y64 = torch.relu(y64)
+    B.check(e1, y64, e, "eager after capture")
+    B.check(got_g, y64, e, "captured (replayed)")
+    clear_conv_workspaces()
