@@ -14,4 +14,5 @@ for c in FETCH_SIZE WRITE_SIZE; do
 done
 python3 tools/pmc_traffic_json.py gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE gpurun_out/r04_pmc_traffic.json \
   gpurun_out/pmcu4_FETCH_SIZE gpurun_out/pmcu4_WRITE_SIZE
+bash tools/lat_ab.sh rf0 rf1 || exit $?
 echo done
