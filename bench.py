@@ -85,6 +85,9 @@ def parse():
     ap.add_argument("--skip-u1", action="store_true")
     ap.add_argument("--skip-config3", action="store_true", help="skip the configs[3] and configs[4] stream legs")
     ap.add_argument("--skip-u4", action="store_true", help="skip the U4 (EVD with mean) timing")
+    ap.add_argument("--share-device", action="store_true",
+                    help="test hook for a one-GPU box: every rank on cuda:0 over gloo (RCCL refuses two ranks on one "
+                         "device), the real GPU path otherwise -- checks the N > 1 code, not its speed")
     ap.add_argument("--dry-run", action="store_true",
                     help="the multi-rank plumbing without a GPU (CPU tests): gloo ranks, each image's result is its "
                          "field's generating keypoints (no voting), then the timed region's barriers, the gather, "
@@ -104,7 +107,7 @@ def launch_ranks(args):
     import socket
     import subprocess
     n = args.gpus
-    if not args.dry_run:
+    if not args.dry_run and not args.share_device:
         have = torch.cuda.device_count()
         if have < n:
             log(f"bench.py --gpus {n}: only {have} GPU(s) visible")
@@ -154,6 +157,11 @@ def setup_dist(args):
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             dist.init_process_group("gloo")
         return ws, rank, torch.device("cpu")
+    if ws > 1 and args.share_device:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+        return ws, rank, torch.device("cuda", 0)
     if ws > 1:
         if torch.cuda.device_count() <= local:
             raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but {torch.cuda.device_count()} GPU(s) visible")

@@ -455,6 +455,9 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_ba
 #ifndef PVC_WINDOW
 #define PVC_WINDOW 0             // 1: stride-1 convolutions on k_conv3x3w (A/B variant; measured slower)
 #endif
+#ifndef PVC_FRAG_AHEAD
+#define PVC_FRAG_AHEAD 0         // 1: a step's fragments all read before its MFMAs (A/B, with PVC_NW=8)
+#endif
 #ifndef PVC_ISSUE_MID
 #define PVC_ISSUE_MID 2          // 0 before the step's MFMAs, 1 after its first half, 2 = 1 for 256-cout tiles only
 #endif
@@ -697,6 +700,29 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
     for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f4v{0.f, 0.f, 0.f, 0.f};
+    // a step half's fragments (kc: 32 of its 64 channels) and its MFMAs
+    auto read_frags = [&](const uint8_t *st, int kc, h8v (&af)[MI], h8v (&bf)[4]) {
+        const int sg = kc * 4 + (lane >> 4);
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) {
+            const int r = wn * (MI * 16) + mi * 16 + (lane & 15);
+            af[mi] = *(const h8v *)(st + conv_granule(r, sg) * 16);
+        }
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const int r = wm * 64 + ni * 16 + (lane & 15);
+            bf[ni] = *(const h8v *)(st + CT * RB + conv_granule(r, sg) * 16);
+        }
+    };
+    auto mfma_frags = [&](const h8v (&af)[MI], const h8v (&bf)[4]) {
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+                acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mi], bf[ni], acc[mi][ni], 0, 0, 0);
+    };
+    (void)read_frags;
+    (void)mfma_frags;
     // kc-th half of a step (32 of its 64 channels)
     auto compute_kc = [&](const uint8_t *st, int kc) {
         {
@@ -738,6 +764,20 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
         const bool nx = s == k0 && k1 - k0 > 1;
 #else
         const bool nx = s + 1 < k1;
+#endif
+#if PVC_FRAG_AHEAD
+        if (true) {
+            // both halves' fragments read before the step's MFMAs (the
+            // second half's reads in flight under the first half's MFMAs;
+            // registers for 8-wave blocks), the next step's loads between
+            const uint8_t *st = lds + buf * STAGE;
+            h8v a0[MI], b0[4], a1[MI], b1[4];
+            read_frags(st, 0, a0, b0);
+            read_frags(st, 1, a1, b1);
+            mfma_frags(a0, b0);
+            if (nx) issue(s + 1, buf ^ 1);
+            mfma_frags(a1, b1);
+        } else
 #endif
         if (PVC_ISSUE_MID == 1 || (PVC_ISSUE_MID == 2 && CT == 256)) {
             // the next step's loads after this step's first 16 MFMAs: the MFMA
@@ -1562,7 +1602,9 @@ ConvSplit conv_split(int64_t pixels, int32_t cout, int32_t ksteps) {
     while (S > 1 && ksteps / S < 4) --S;          // parts of at least 4 K-steps
     if (S < 2) return ConvSplit{(int)ntiles, 1, 0, 0};
     const int64_t tb = (rem * 4 + 255) / 256 * 256;
-    const int64_t per = (int64_t)S * (wide ? 16 : 8) * (64 * kNW) * 16;   // one tile's partials
+    // one tile's partials: its CT x 256 f32 sums (each of the 64 kNW threads
+    // holds CT / kNW 16-byte groups), per part
+    const int64_t per = (int64_t)S * (wide ? kCT : 128) * kPT * 4;
     return ConvSplit{(int)(ntiles - rem), S, tb, tb + rem * per};
 }
 }  // namespace

@@ -53,3 +53,26 @@ def test_failing_rank_stops_launch():
     # stop the others and return non-zero instead of waiting
     p = _run("--gpus", "2", "--skip-cpu", "--steps", "0")
     assert p.returncode != 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_launcher_two_ranks_on_the_device():
+    """The real GPU path at N = 2 on a one-GPU box: bench.py starts two ranks
+    that share cuda:0 over gloo (--share-device; RCCL refuses two ranks on one
+    device) and run the headline stream, configs[3] and configs[4] legs,
+    graph capture and replay included, through the sharded gather; one JSON
+    line with n_gpus 2 and every gathered image in its stream slot."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--share-device", "--steps", "2",
+           "--warmup", "1", "--per-step", "16", "--fields", "4", "--skip-e2e", "--skip-u1", "--skip-u4",
+           "--skip-cpu"]
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=580)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["stream_order_ok"]
+    assert line["config"]["stream_images"] == 2 * 2 * 16
+    assert line["stream_config3"]["n_gpus"] == 2 and line["stream_config3"]["zeros_path_ok"]
+    assert line["stream_config4"]["n_gpus"] == 2 and line["stream_config4"]["covariances_finite"]
