@@ -16,8 +16,8 @@
 // pixel patch of fm, 10 rows of the image) loaded into registers while this
 // tile convolves.  Per tile the block builds the convolution's input halo
 // (10 x 34 pixels x 40 channels fp16: 32 upsampled, the image's 3, 5 zero) in
-// LDS -- the x2 bilinear blend separably, column blends once per (fm row,
-// halo column), then row blends, in packed fp16 -- and each wave computes two
+// LDS -- the x2 bilinear blend per halo pixel straight from the patch, two
+// column blends then a row blend in packed fp16 -- and each wave computes two
 // rows of 32 pixels: a 3x3 convolution as [32 out x 368 k] x [368 k x 32
 // pixels] on v_mfma_f32_32x32x16_f16 (k = tap x 40 channels, 23 MFMAs per row;
 // the A fragments -- the weights -- stay in registers for the whole launch,
@@ -69,7 +69,6 @@ constexpr int kPatchIt = (kPatchChunks + 255) / 256;
 constexpr int kImgDw = 52;
 constexpr int kImgWords = kHR * kImgDw;
 constexpr int kImgIt = (kImgWords + 255) / 256;
-constexpr int kTcolTasks = kPR * kHC * 4;         // column blends: (fm row, halo column, 8 channels)
 
 struct TailArgs {
     const _Float16 *fm;    // [N][Hin][Win][32]
@@ -114,40 +113,50 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t image_rsrc(const void *base, i
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)bytes, 0x00020000);
 }
 
-// global loads of a tile's fm patch and image rows into registers (buffer
-// loads: rows past the map read 0, columns past it read the next row -- the
-// halo build never uses either), so nothing waits on them until the next
-// tile's halo build.  pk / ik: the thread's tile-independent chunk coordinates.
-__device__ __forceinline__ void fetch(const TailArgs &a, int tile, const int (&pk)[kPatchIt],
-                                      const int (&ik)[kImgIt], h8 (&pre)[kPatchIt], uint32_t (&pimg)[kImgIt]) {
+// a tile's fm patch and image rows, straight to LDS (buffer loads to LDS, 16
+// and 4 bytes a lane at lane-linear addresses: patch chunk c at byte 16 c,
+// image dword w at byte 4 w; rows past the map read 0, columns past it read
+// the next row -- the halo build never uses either).  Issued once the halo
+// is built, so they land during this tile's convolution and nothing holds
+// registers for them (round 4; before: loads into 15 VGPRs and an LDS store
+// phase, which kept the kernel at 2 blocks per CU).
+__device__ __forceinline__ void fetch(const TailArgs &a, int tile, _Float16 *patch, uint32_t *imgs) {
     int b, y0, x0, ly0, lx0;
     tile_coords(a, tile, b, y0, x0, ly0, lx0);
+    const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
     const int64_t fbytes = (int64_t)a.Hin * a.Win * 64;
     const __amdgpu_buffer_rsrc_t fr = image_rsrc(a.fm + (int64_t)b * a.Hin * a.Win * 32, fbytes);
     const int base = (ly0 * a.Win + lx0) * 64;
 #pragma unroll
     for (int i = 0; i < kPatchIt; ++i) {
-        const int off = base + (pk[i] >> 16) * a.Win * 64 + (pk[i] & 0xffff);
-        pre[i] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(fr, off, 0, 0));
+        const int c0 = 256 * i + 64 * wid, c = c0 + lane;     // the wave's first chunk, the lane's
+        if (c0 < kPatchChunks && c < kPatchChunks) {
+            const int pp = c >> 2, pr = pp / kPC;
+            const int off = base + pr * a.Win * 64 + (pp - pr * kPC) * 64 + 16 * (c & 3);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(fr, (__attribute__((address_space(3))) void *)(patch + 8 * c0),
+                                                     16, off, 0, 0, 0);
+        }
     }
     const int64_t ibytes = (int64_t)a.H * a.W * 6;
     const __amdgpu_buffer_rsrc_t ir = image_rsrc(a.img + (int64_t)b * a.H * a.W * 3, ibytes);
     const int ibase = ((y0 - 1) * a.W * 3 / 2 + x0 * 3 / 2 - 2) * 4;
 #pragma unroll
     for (int i = 0; i < kImgIt; ++i) {
-        const int off = ibase + (ik[i] >> 8) * a.W * 6 + (ik[i] & 255) * 4;
-        pimg[i] = __builtin_amdgcn_raw_buffer_load_b32(ir, off, 0, 0);
+        const int w0 = 256 * i + 64 * wid, w = w0 + lane;
+        if (w0 < kImgWords && w < kImgWords) {
+            const int r = w / kImgDw;
+            const int off = ibase + r * a.W * 6 + (w - r * kImgDw) * 4;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(ir, (__attribute__((address_space(3))) void *)(imgs + w0), 4,
+                                                     off, 0, 0, 0);
+        }
     }
 }
 
 // per-thread fixed task geometry of the halo build (tile independent): the
-// 136 (halo column, 8-channel group) pairs c = 4 hx + q over the halo's 10
-// rows (row blends) and the patch's 7 rows (column blends)
+// 136 (halo column, 8-channel group) pairs c = 4 hx + q over the halo's 10 rows
 struct Geo {
-    int rc0, rhy0, rc1, rhy1;    // row blends: rows rhy0 .. rhy0 + 4 of column task rc0; + (rc1, rhy1) if rx
+    int rc0, rhy0, rc1, rhy1;    // rows rhy0 .. rhy0 + 4 of column task rc0; + (rc1, rhy1) if rx
     bool rx;
-    int tc0, tr0, tn0, tc1, tr1;  // column blends: rows tr0 .. tr0 + tn0 - 1 of tc0; + (tc1, tr1) if tx
-    bool tx;
 };
 
 __device__ __forceinline__ Geo make_geo(int t) {
@@ -158,12 +167,6 @@ __device__ __forceinline__ Geo make_geo(int t) {
     g.rx = t < 80;
     g.rc1 = 120 + (t & 15);
     g.rhy1 = 5 + (t >> 4);
-    g.tc0 = g.rc0;                     // 136 threads x rows 0..3, 120 x rows 4..6; the last 16 columns
-    g.tr0 = lo ? 0 : 4;                // of rows 4..6 by threads 136..183
-    g.tn0 = lo ? 4 : 3;
-    g.tx = t >= 136 && t < 184;
-    g.tc1 = 120 + ((t - 136) & 15);
-    g.tr1 = 4 + ((t - 136) >> 4);
     return g;
 }
 
@@ -188,113 +191,104 @@ __device__ __forceinline__ ColW col_weights(const TailArgs &a, int c, int x0, in
     return r;
 }
 
-__device__ __forceinline__ void col_blend(const _Float16 *patch, _Float16 *tcol, const ColW &w, int c, int r) {
-    const _Float16 *p = patch + r * (kPC * 32) + w.poff;
-    const h8 A = *(const h8 *)p, B = *(const h8 *)(p + w.dp);
-    *(h8 *)(tcol + r * (kHC * 32) + 8 * c) = __builtin_elementwise_fma(B, (h8)w.w1, A * (h8)w.w0);
-}
-
-__device__ __forceinline__ void row_blend(const TailArgs &a, const _Float16 *tcol, _Float16 *halo, int c, int hy,
-                                          bool colok, int y0, int ly0) {
+// halo pixel (row hy, column task c = 4 hx + q): the column blends of its
+// two source rows of the patch, then the row blend (zero outside the image).
+// Round 4: straight from the patch -- a column blend is recomputed for each
+// of the ~3 halo rows that use it (1.8x the blend arithmetic) instead of
+// going through an LDS intermediate with its own phase and barrier; the
+// fp16 expressions, and so the values, are those of the separable form.
+// (Measured: a branch-free form sharing a thread's four column blends over
+// its five rows, with bit-mask picks, was 6 % slower -- the picks cost more
+// VALU than the reads they save.)
+__device__ __forceinline__ void halo_blend(const TailArgs &a, const _Float16 *patch, _Float16 *halo, const ColW &w,
+                                           int c, int hy, bool colok, int y0, int ly0) {
     const int oy = y0 - 1 + hy;
     h8 v = {};
     if (colok && oy >= 0 && oy < a.H) {
         const float h1r = a.rh * (float)oy;
         const int h1 = (int)h1r;
-        const int dh = h1 < a.Hin - 1 ? kHC * 32 : 0;
+        const int dh = h1 < a.Hin - 1 ? kPC * 32 : 0;
         const float h1l = h1r - (float)h1;
-        const _Float16 *tp = tcol + (h1 - ly0) * (kHC * 32) + 8 * c;
-        const h8 c0 = *(const h8 *)tp, c1 = *(const h8 *)(tp + dh);
+        const _Float16 *p = patch + (h1 - ly0) * (kPC * 32) + w.poff;
+        const h8 A = *(const h8 *)p, B = *(const h8 *)(p + w.dp);
+        const h8 C = *(const h8 *)(p + dh), D = *(const h8 *)(p + dh + w.dp);
+        const h8 c0 = __builtin_elementwise_fma(B, (h8)w.w1, A * (h8)w.w0);
+        const h8 c1 = __builtin_elementwise_fma(D, (h8)w.w1, C * (h8)w.w0);
         v = __builtin_elementwise_fma(c1, (h8)(_Float16)h1l, c0 * (h8)(_Float16)(1.f - h1l));
     }
     *(h8 *)(halo + hy * (kHC * kCP) + (c >> 2) * kCP + 8 * (c & 3)) = v;
 }
 
+#ifndef PVT_WPE
+#define PVT_WPE 3            // waves per SIMD the tail's registers are sized for (blocks of 4 waves per CU)
+#endif
+#ifndef PVT_WREG
+#define PVT_WREG 12          // k-steps whose weights stay in registers (cout <= 32; 2 fewer above); the rest in LDS
+#endif
+
 template <int COUT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_decoder_tail(TailArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVT_WPE, PVT_WPE))) void k_decoder_tail(TailArgs a) {
     constexpr int MT = (COUT + 31) / 32;
+    constexpr int kWReg = MT == 1 ? PVT_WREG : PVT_WREG - 2, kWLds = kKS - kWReg;
+    static_assert(kWReg >= 1 && kWLds >= 0, "PVT_WREG in 3 .. 23");
     __shared__ alignas(16) _Float16 halo[kHaloPx * kCP];
     __shared__ alignas(16) _Float16 patch[kPatchChunks * 8];
-    __shared__ alignas(16) _Float16 tcol[kTcolTasks * 8];
     __shared__ alignas(16) uint32_t imgs[kImgWords];
     __shared__ alignas(16) _Float16 bias[32 + 32 * MT];
+    __shared__ alignas(16) h8 wlds[kWLds > 0 ? kWLds * 64 : 1];   // k-steps kWReg.. : [s][lane]
     const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
     const int n = lane & 31, h = lane >> 5;
-    // the wave's A fragments for the whole launch: lane (out r = n, half h)
-    // holds w1[r][16 s + 8 h .. + 8] for k-step s
-    h8 wa[kKS];
+    // the A fragments for the whole launch: lane (out r = n, half h) takes
+    // w1[r][16 s + 8 h .. + 8] for k-step s -- the first kWReg k-steps' from
+    // the wave's registers, the rest from LDS (one conflict-free ds_read_b128
+    // per k-step, shared by the wave's two rows).  All 23 in registers held the
+    // kernel at 2 blocks per CU (224 VGPRs); 12 (10 for the 44-output head: 5 spilled VGPRs)
+    // leave it 3 (round 4).
+    h8 wa[kWReg];
 #pragma unroll
-    for (int s = 0; s < kKS; ++s) wa[s] = *(const h8 *)(a.w1 + n * kK + 16 * s + 8 * h);
+    for (int s = 0; s < kWReg; ++s) wa[s] = *(const h8 *)(a.w1 + n * kK + 16 * s + 8 * h);
+    for (int i = (int)threadIdx.x; i < kWLds * 64; i += 256) {
+        const int s = kWReg + (i >> 6), l = i & 63;
+        wlds[i] = *(const h8 *)(a.w1 + (l & 31) * kK + 16 * s + 8 * (l >> 5));
+    }
     h8 wb[MT][2];
 #pragma unroll
     for (int t = 0; t < MT; ++t)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) wb[t][s2] = *(const h8 *)(a.w2 + ((t * 2 + s2) * 32 + n) * 16 + 8 * h);
-    // the weights are in registers before the tile loop (vmcnt 0): the loop's
-    // only outstanding loads are then the next tile's prefetch, which nothing
-    // waits for until the next iteration
+    // the weights are in registers before the tile loop (vmcnt 0)
     __builtin_amdgcn_s_waitcnt(0x0F70);
     // the biases, fp16: conv rows [0, 32), head outputs [32, 32 + 32 MT)
     for (int i = (int)threadIdx.x; i < 32 + 32 * MT; i += 256)
         bias[i] = i < 32 ? (_Float16)a.b1[i] : (i - 32 < COUT ? (_Float16)a.b2[i - 32] : (_Float16)0.f);
-    int pk[kPatchIt], ik[kImgIt];
-#pragma unroll
-    for (int i = 0; i < kPatchIt; ++i) {
-        const int c = min((int)threadIdx.x + 256 * i, kPatchChunks - 1);
-        const int pp = c >> 2, pr = pp / kPC;
-        pk[i] = (pr << 16) | ((pp - pr * kPC) * 64 + 16 * (c & 3));
-    }
-#pragma unroll
-    for (int i = 0; i < kImgIt; ++i) {
-        const int w = min((int)threadIdx.x + 256 * i, kImgWords - 1);
-        const int r = w / kImgDw;
-        ik[i] = (r << 8) | (w - r * kImgDw);
-    }
     const Geo g = make_geo((int)threadIdx.x);
-    // next tile's inputs, fetched during this tile's convolution
-    h8 pre[kPatchIt];
-    uint32_t pimg[kImgIt];
+    // the next tile's inputs are fetched during this tile's convolution
     int tile = (int)blockIdx.x;
-    if (tile < a.ntiles) fetch(a, tile, pk, ik, pre, pimg);
+    if (tile < a.ntiles) fetch(a, tile, patch, imgs);
     for (int it = 0; tile < a.ntiles; tile += (int)gridDim.x, ++it) {
         (void)it;
         PVT_STAMP(0);
         int b, y0, x0, ly0, lx0;
         tile_coords(a, tile, b, y0, x0, ly0, lx0);
-        // patch / imgs were last read before the previous tile's second barrier
-#pragma unroll
-        for (int i = 0; i < kPatchIt; ++i) {
-            const int c = (int)threadIdx.x + 256 * i;
-            if (c < kPatchChunks) *(h8 *)(patch + 8 * c) = pre[i];
-        }
-#pragma unroll
-        for (int i = 0; i < kImgIt; ++i) {
-            const int w = (int)threadIdx.x + 256 * i;
-            if (w < kImgWords) imgs[w] = pimg[i];
-        }
+        // this wave's patch / image loads have landed (vmcnt 0: its last tile's
+        // stores are out too), then every wave's; every wave is also past the
+        // previous tile's convolution (halo reads)
+        __builtin_amdgcn_s_waitcnt(0x0F70);
         PVT_STAMP(1);
         __syncthreads();
         PVT_STAMP(2);
-        // ---- halo: pixel (y0 - 1 + hy, x0 - 1 + hx).  x2 bilinear, align_corners, separably:
-        // column blends t = w0l A + w1l B per (fm row, halo column, 8 channels) ----
-#ifndef PVT_SKIP_HALO
-        {
-            const ColW w0 = col_weights(a, g.tc0, x0, lx0);
-            for (int i = 0; i < g.tn0; ++i) col_blend(patch, tcol, w0, g.tc0, g.tr0 + i);
-            if (g.tx) col_blend(patch, tcol, col_weights(a, g.tc1, x0, lx0), g.tc1, g.tr1);
-        }
-#endif
         PVT_STAMP(3);
-        __syncthreads();   // also: every wave is past the previous tile's convolution (halo reads)
         PVT_STAMP(4);
+        // ---- halo: pixel (y0 - 1 + hy, x0 - 1 + hx).  x2 bilinear, align_corners:
+        // column blends t = w0l A + w1l B of fm rows h1, h1 + 1, then h0l t(h1) + h1l t(h1 + 1) ----
 #ifndef PVT_SKIP_HALO
         {
-            // row blends h0l t(h1) + h1l t(h1 + 1) per (halo pixel, 8 channels)
             const int ox0 = x0 - 1 + (g.rc0 >> 2), ox1 = x0 - 1 + (g.rc1 >> 2);
             const bool ok0 = ox0 >= 0 && ox0 < a.W, ok1 = ox1 >= 0 && ox1 < a.W;
+            const ColW w0 = col_weights(a, g.rc0, x0, lx0);
 #pragma unroll
-            for (int i = 0; i < 5; ++i) row_blend(a, tcol, halo, g.rc0, g.rhy0 + i, ok0, y0, ly0);
-            if (g.rx) row_blend(a, tcol, halo, g.rc1, g.rhy1, ok1, y0, ly0);
+            for (int i = 0; i < 5; ++i) halo_blend(a, patch, halo, w0, g.rc0, g.rhy0 + i, ok0, y0, ly0);
+            if (g.rx) halo_blend(a, patch, halo, col_weights(a, g.rc1, x0, lx0), g.rc1, g.rhy1, ok1, y0, ly0);
             // the image's channels 32..39 (3 + 5 zero)
             for (int p = (int)threadIdx.x; p < kHaloPx; p += 256) {
                 const int hy = p / kHC, hx = p - hy * kHC;
@@ -313,7 +307,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         PVT_STAMP(5);
         __syncthreads();
         PVT_STAMP(6);
-        if (tile + (int)gridDim.x < a.ntiles) fetch(a, tile + (int)gridDim.x, pk, ik, pre, pimg);
+        // patch / imgs are free (read only by the halo build)
+        if (tile + (int)gridDim.x < a.ntiles) fetch(a, tile + (int)gridDim.x, patch, imgs);
         // ---- the wave's two output rows: 3x3 convolution on the matrix cores ----
         f16x acc[2];
 #pragma unroll
@@ -332,8 +327,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             } else {
                 bf[0] = bf[1] = h8{};
             }
+            const h8 af = s < kWReg ? wa[s < kWReg ? s : 0] : wlds[(s - kWReg) * 64 + lane];
 #pragma unroll
-            for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa[s], bf[r], acc[r], 0, 0, 0);
+            for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf[r], acc[r], 0, 0, 0);
         }
 #else
         acc[0][0] = (float)halo[threadIdx.x];
@@ -1574,7 +1570,7 @@ extern "C" int pv_decoder_tail_f16(const void *fm, const void *img, const void *
 #ifdef PVT_TRACE
     a.trace = g_tail_trace;
 #endif
-    const int64_t grid = std::min<int64_t>(nt, 2ll * cu_count_dec());   // persistent: 2 blocks per CU
+    const int64_t grid = std::min<int64_t>(nt, (int64_t)PVT_WPE * cu_count_dec());   // persistent: PVT_WPE blocks per CU
     hipStream_t s = (hipStream_t)stream;
     if (cout == 20) k_decoder_tail<20><<<(unsigned)grid, 256, 0, s>>>(a);
     else k_decoder_tail<44><<<(unsigned)grid, 256, 0, s>>>(a);

@@ -20,7 +20,7 @@ wts = decoder_tail_weights(c0, c1)
 lib = _lib.load()
 fn = lib.pv_debug_set_tail_trace
 fn.argtypes = [ctypes.c_void_p]
-nblk = 512
+nblk = 1024                                              # >= the grid (PVT_WPE blocks per CU)
 tr = torch.zeros(nblk * 8 * 4 * 8, dtype=torch.int64, device="cuda")
 for _ in range(3):
     decoder_tail(fm, img, wts)
@@ -29,7 +29,10 @@ decoder_tail(fm, img, wts)
 torch.cuda.synchronize()
 fn(None)
 t = tr.cpu().numpy().reshape(nblk, 8, 4, 8).astype(np.float64)
-names = ["top->patch stored", "barrier1", "col blends", "barrier2", "row+img blends", "barrier3",
+t = t[(t[:, 6, :, 7] > 0).all(axis=1)]                   # blocks of the grid with >= 7 tiles
+# round 4 layout: 0 top, 1 after the wait for the fetch, 2 after barrier 1,
+# (3, 4 = 2), 5 after the halo build, 6 after barrier 2, 7 after fetch + conv
+names = ["wait fetch (vmcnt)", "barrier1", "-", "-", "halo build", "barrier2",
          "fetch+conv", "epilogue->next top"]
 d = np.diff(t, axis=3)                                   # phases 0..6
 nxt = t[:, 1:, :, 0] - t[:, :-1, :, 7]                   # epilogue (+loop) to next tile's top
