@@ -454,6 +454,9 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_ba
 #ifndef PVC_FRAG_AHEAD
 #define PVC_FRAG_AHEAD 0         // 1: a step's fragments all read before its MFMAs (A/B, with PVC_NW=8)
 #endif
+#ifndef PVC_PRIO
+#define PVC_PRIO 0               // 1: s_setprio(1) around each MFMA cluster (A/B)
+#endif
 #ifndef PVC_ISSUE_MID
 #define PVC_ISSUE_MID 2          // 0 before the step's MFMAs, 1 after its first half, 2 = 1 for 256-cout tiles only
 #endif
@@ -738,11 +741,17 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
 #pragma unroll
             for (int mi = 0; mi < MI; ++mi) acc[mi][0][0] += (float)af[mi][0] + (float)bf[mi & 3][1];
 #else
+#if PVC_PRIO
+            __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
             for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
                 for (int ni = 0; ni < 4; ++ni)
                     acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mi], bf[ni], acc[mi][ni], 0, 0, 0);
+#if PVC_PRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
 #endif
         }
     };
