@@ -432,19 +432,22 @@ def test_head_matches_torch(cout, dtype, device):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cout", [20, 44])
-@pytest.mark.parametrize("hw", [(13, 21), (60, 80)])
+@pytest.mark.parametrize("hw", [(13, 21, 2), (60, 80, 2), (120, 160, 8)])
 def test_decoder_tail_matches_torch(cout, hw, device):
     """pv_decoder_tail_f16 (up2storaw + cat([fm, x]) + convraw, MR:75-79, one
     matrix-core pass) against ATen's unfused fp16 ops on the same inputs:
     F.interpolate + torch.cat + the 3x3 conv + bias + LeakyReLU + the 1x1
     conv.  Both sum in f32 and round the 3x3 output to fp16 (MIOpen in
     another order), so the outputs agree within a couple of fp16 roundings
-    of the head's scale; ragged tiles (13 x 21 -> 26 x 42) included."""
+    of the head's scale; ragged tiles (13 x 21 -> 26 x 42) included.  The
+    batch-8 case has 2,400 tiles for the 3 x CUs persistent blocks, so every
+    block runs several tiles: the next tile's patch and image rows land in
+    LDS (buffer loads to LDS) while the block convolves the current one."""
     from pvnet_amd.network import decoder_tail, decoder_tail_weights
     F = torch.nn.functional
     g = torch.Generator().manual_seed(cout + hw[0])
     cl = torch.channels_last
-    n, (h, w) = 2, hw
+    h, w, n = hw
     fm = (torch.randn(n, 32, h, w, generator=g) * 2).to(device, torch.float16).contiguous(memory_format=cl)
     img = torch.randn(n, 3, 2 * h, 2 * w, generator=g).to(device, torch.float16).contiguous(memory_format=cl)
     c0 = torch.nn.Conv2d(35, 32, 3, 1, 1).to(device)
@@ -683,19 +686,20 @@ def test_conv3x3_weight_with_downsample():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("hw", [(13, 21), (60, 80)])
+@pytest.mark.parametrize("hw", [(13, 21, 2), (60, 80, 2), (60, 80, 8)])
 def test_decoder_conv2s_matches_torch(hw, device):
     """pv_decoder_conv2s_f16 (up4sto2s + cat([fm, x2s]) + conv2s, MR:43-51, one
     matrix-core pass) against ATen's unfused fp16 ops on the same inputs:
     F.interpolate + torch.cat + the 3x3 conv + bias + LeakyReLU.  The blend's
     fp16 weights and the summation order differ, so the outputs agree within
     a couple of fp16 roundings of the convolution's scale; ragged tiles
-    (26 x 42) included."""
+    (26 x 42) included; batch 8 at 120 x 160 has more tiles than persistent
+    blocks (the next tile's inputs prefetched during a tile)."""
     from pvnet_amd.network import decoder_conv2s, decoder_conv2s_weights
     F = torch.nn.functional
     g = torch.Generator().manual_seed(hw[0] * 31 + hw[1])
     cl = torch.channels_last
-    n, (h, w) = 2, hw
+    h, w, n = hw
     fm = (torch.randn(n, 64, h, w, generator=g) * 2).to(device, torch.float16).contiguous(memory_format=cl)
     skip = torch.randn(n, 64, 2 * h, 2 * w, generator=g).to(device, torch.float16).contiguous(memory_format=cl)
     c = torch.nn.Conv2d(128, 32, 3, 1, 1).to(device)
@@ -743,15 +747,16 @@ def test_decoder_conv_weight_layouts():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("hw", [(13, 21), (60, 80)])
+@pytest.mark.parametrize("hw", [(13, 21, 2), (60, 80, 2), (60, 80, 8)])
 def test_decoder_conv4s_matches_torch(hw, device):
     """pv_decoder_conv4s_f16 (up8sto4s + cat([fm, x4s]) + conv4s, MR:35-43)
-    against ATen's unfused fp16 ops; tolerance as the conv2s test."""
+    against ATen's unfused fp16 ops; tolerance as the conv2s test (batch 8:
+    several tiles per persistent block)."""
     from pvnet_amd.network import decoder_conv4s, decoder_conv4s_weights
     F = torch.nn.functional
     g = torch.Generator().manual_seed(hw[0] * 17 + hw[1])
     cl = torch.channels_last
-    n, (h, w) = 2, hw
+    h, w, n = hw
     fm = (torch.randn(n, 128, h, w, generator=g) * 2).to(device, torch.float16).contiguous(memory_format=cl)
     skip = torch.randn(n, 64, 2 * h, 2 * w, generator=g).to(device, torch.float16).contiguous(memory_format=cl)
     c = torch.nn.Conv2d(192, 64, 3, 1, 1).to(device)
@@ -886,19 +891,22 @@ def test_conv64_weight_layout():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["relu_120x160", "res_120x160", "none_ragged_13x37"])
+@pytest.mark.parametrize("case", ["relu_120x160", "res_120x160", "none_ragged_13x37", "res_120x160x8"])
 def test_conv64_matches_torch(case, device):
     """pv_conv64_f16 (layer1's 64 -> 64 3x3 convolutions with bias, residual
     and ReLU, RN:21-70) against MIOpen's fp16 convolution + ATen's bias /
-    residual / ReLU; tolerance as the conv3x3 test; ragged tiles included."""
+    residual / ReLU; tolerance as the conv3x3 test; ragged tiles included;
+    `x8`: batch 8, more tiles than persistent blocks (the next tile's halo
+    prefetched during a tile)."""
     from pvnet_amd.network import conv64, conv64_weights
     F = torch.nn.functional
     kind, hw = case.split("_")[0], case.split("_")[-1]
-    h, w = (int(v) for v in hw.split("x"))
+    dims = [int(v) for v in hw.split("x")]
+    h, w, n = dims[0], dims[1], (dims[2] if len(dims) > 2 else 2)
     g = torch.Generator().manual_seed(h * w)
     cl = torch.channels_last
-    x = torch.randn(2, 64, h, w, generator=g).to(device, torch.float16).contiguous(memory_format=cl)
-    res = torch.randn(2, 64, h, w, generator=g).to(device, torch.float16).contiguous(memory_format=cl)
+    x = torch.randn(n, 64, h, w, generator=g).to(device, torch.float16).contiguous(memory_format=cl)
+    res = torch.randn(n, 64, h, w, generator=g).to(device, torch.float16).contiguous(memory_format=cl)
     c = torch.nn.Conv2d(64, 64, 3, 1, 1).to(device)
     with torch.no_grad():
         c.weight.copy_(torch.randn(64, 64, 3, 3, generator=g) / 24)
