@@ -70,9 +70,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--per-step", type=int, default=128,
+    ap.add_argument("--per-step", type=int, default=1024,
                     help="images per GPU per step: one step = one replay of a hipGraph that votes this many "
-                         "batch-1 frames (configs[1]), `--inflight` of them at a time on separate streams")
+                         "batch-1 frames (configs[1]), `--inflight` of them at a time on separate streams (the "
+                         "graph's fork and join cost ~0.17 ms per replay: 128 frames per step 49.2k images/s, "
+                         "512 51k, 1024 51.6k, 2048 52.3k on one box; DESIGN.md 7)")
     ap.add_argument("--fields", type=int, default=64,
                     help="distinct resident S(seed) fields per GPU the stream cycles through (64 x 24.6 MB: the "
                          "~5 MB each image reads, x64, exceeds the 256 MiB Infinity Cache, so inputs come from HBM)")

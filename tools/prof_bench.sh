@@ -13,6 +13,8 @@ grep '^{' gpurun_out/bench_prof.log | tail -1 > gpurun_out/bench_prof.json
 python3 tools/u1_trace_summary.py gpurun_out/prof_bench/bench_kernel_trace.csv gpurun_out/bench_prof.json gpurun_out/u1_timed_launches.json
 python3 tools/u4_trace_summary.py gpurun_out/prof_bench/bench_kernel_trace.csv gpurun_out/bench_prof.json gpurun_out/u4_timed_launches.json
 python3 tools/kernel_phases.py gpurun_out/prof_bench/bench_kernel_trace.csv gpurun_out/kernel_phases.json > /dev/null 2>&1 || true
+# the full trace (~1M rows at 1,024 frames per step) stays on the box: its summaries above are what is kept
+rm -f gpurun_out/prof_bench/bench_kernel_trace.csv
 if [ -n "$PMC" ]; then
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 400 rocprofv3 --kernel-include-regex "k_vote|k_compact|k_fg_count|k_refine|k_hyp_gen|k_front" --pmc $c -T --output-format csv \
