@@ -61,6 +61,31 @@ def pmc_traffic(kernel):
         return None
 
 
+_STREAMS = []
+_GRAPHS = []
+
+
+def new_stream(dev):
+    """A HIP stream kept alive for the whole process: the captured graphs
+    outlive the functions that capture them, and no stream a graph was
+    captured on is destroyed before that graph (a host SIGSEGV in a probe
+    that built and dropped many stream graphs in one process was the reason
+    to rule that order out)."""
+    st = torch.cuda.Stream(device=dev)
+    _STREAMS.append(st)
+    return st
+
+
+def new_graph():
+    """A hipGraph kept alive for the whole process, like the streams: no
+    graph is destroyed between another graph's capture and launch (a probe
+    that captured, replayed and dropped several large stream graphs in one
+    process died in a later graph's first replay, intermittently)."""
+    g = torch.cuda.CUDAGraph()
+    _GRAPHS.append(g)
+    return g
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -224,10 +249,10 @@ def graph_stream(args, ws, rank, dev, steps, seed_base, vote, parts, per_step=No
     mine = D.shard(n_images, rank, ws)             # this rank's images, in stream order
     assert len(mine) == K * M
     NL = max(1, args.inflight)
-    lanes = [torch.cuda.Stream(device=dev) for _ in range(NL)]
+    lanes = [new_stream(dev) for _ in range(NL)]
     outs = [torch.zeros((M,) + tuple(sh), dtype=dt, device=dev) for sh, dt in parts]
     local = [torch.zeros((K * M,) + tuple(sh), dtype=dt, device=dev) for sh, dt in parts]
-    s = torch.cuda.Stream(device=dev)
+    s = new_stream(dev)
 
     def step_body(seed0):
         for ln in lanes:
@@ -243,7 +268,7 @@ def graph_stream(args, ws, rank, dev, steps, seed_base, vote, parts, per_step=No
         for w in range(max(1, args.warmup)):
             step_body(seed_base + 1000 * w + rank * 7_919)
     torch.cuda.synchronize()
-    graph = torch.cuda.CUDAGraph()
+    graph = new_graph()
     with torch.cuda.stream(s):
         with torch.cuda.graph(graph, stream=s):
             step_body(seed_base + 3 + rank * 1_000_003)
@@ -392,7 +417,7 @@ def main():
     vote_ms, compact_ms = time_vote_kernel(rvg, segs, vers, args.hn, seeds, works[0], out_step, s)
     # per-image latency: 32 images one after another on one stream (rotating fields)
     NLAT = 32
-    lat = torch.cuda.CUDAGraph()
+    lat = new_graph()
     with torch.cuda.stream(s):
         with torch.cuda.graph(lat, stream=s):
             for j in range(NLAT):
@@ -583,14 +608,14 @@ def measure_u1(dev, hn=512, reps=100):
     idxs = torch.randint(0, tn, (hn, VN, 2), dtype=torch.int32, device=dev)
     hyp = rv.generate_hypothesis(direct, coords, idxs)
     inl = torch.empty((hn, VN, tn), dtype=torch.uint8, device=dev)
-    s = torch.cuda.Stream(device=dev)
+    s = new_stream(dev)
     with torch.cuda.stream(s):
         for _ in range(5):
             rv.voting_for_hypothesis_dense(direct, coords, hyp, inl, 0.99)
     torch.cuda.synchronize()
     # `reps` launches back to back in one hipGraph (no host gaps between
     # them: the device time per launch that rocprof's kernel trace measures)
-    g = torch.cuda.CUDAGraph()
+    g = new_graph()
     with torch.cuda.stream(s):
         with torch.cuda.graph(g, stream=s):
             for _ in range(reps):
@@ -636,7 +661,7 @@ def measure_u4(dev, reps=20):
     mean = torch.from_numpy(f["keypoints"].astype(np.float32)[None]).to(dev)
     work = rvg.VotingWorkspace()
     L = _lib.load()
-    s = torch.cuda.Stream(device=dev)
+    s = new_stream(dev)
     ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(5)) for _ in range(reps + 3)]
     cov = torch.empty((1, VN, 2, 2), dtype=torch.float32, device=dev)
     with torch.cuda.stream(s):
@@ -692,12 +717,12 @@ def measure_batch(dev, b=32, hn=512, steps=10):
     ver = torch.from_numpy(np.concatenate([f["vertex"] for f in fs])).to(dev)
     work = rvg.VotingWorkspace()
     out = torch.zeros((steps, b, VN, 2), dtype=torch.float32, device=dev)
-    s = torch.cuda.Stream(device=dev)
+    s = new_stream(dev)
     with torch.cuda.stream(s):
         for k in range(3):
             rvg.ransac_voting_layer_v3_from_network(seg, ver, hn, _seed=k, _workspace=work, out=out[0])
     torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
+    g = new_graph()
     with torch.cuda.stream(s):
         with torch.cuda.graph(g, stream=s):
             for k in range(steps):
@@ -800,11 +825,11 @@ def measure_pose(dev, b=32, steps=5):
         mean, cov = rvg.estimate_voting_distribution_with_mean(mask, vertex, mean, _workspace=w2, _seed=12)
         return eu.uncertainty_pnp_batch(mean, cov, tp3, tK, mode="cov", diag=pd)
     pd = {}
-    s = torch.cuda.Stream(device=dev)
+    s = new_stream(dev)
     with torch.cuda.stream(s):
         Rt = once()
     torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
+    g = new_graph()
     with torch.cuda.stream(s):
         with torch.cuda.graph(g, stream=s):
             Rt = once()
@@ -853,12 +878,12 @@ def measure_e2e_config4(dev, batch=32, iters=10):
             mean, cov = rvg.estimate_voting_distribution_with_mean(mask, vertex, mean, _workspace=w2, _seed=14)
             return eu.uncertainty_pnp_batch(mean, cov, p3, K, mode="cov")
 
-    s = torch.cuda.Stream(device=dev)
+    s = new_stream(dev)
     with torch.cuda.stream(s):
         for _ in range(2):
             once()
     torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
+    g = new_graph()
     with torch.cuda.stream(s):
         with torch.cuda.graph(g, stream=s):
             Rt = once()
@@ -925,12 +950,12 @@ def measure_e2e(dev, half=False, batch=1, iters=30, hn=512, form=None):
         return rvg.ransac_voting_layer_v3_from_network(sg, v, hn, _workspace=ws, max_num=30000, _seed=7, out=out)
 
     def timed(fn):
-        s = torch.cuda.Stream(device=dev)
+        s = new_stream(dev)
         with torch.cuda.stream(s):
             for _ in range(3):
                 fn()
         torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
+        g = new_graph()
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s):
                 fn()
