@@ -23,6 +23,7 @@ Prints ONE JSON line on rank 0 (contract in the task statement).
 from __future__ import annotations
 
 import argparse
+import faulthandler
 import json
 import os
 import sys
@@ -62,28 +63,25 @@ def pmc_traffic(kernel):
 
 
 _STREAMS = []
-_GRAPHS = []
 
 
 def new_stream(dev):
-    """A HIP stream kept alive for the whole process: the captured graphs
-    outlive the functions that capture them, and no stream a graph was
-    captured on is destroyed before that graph (a host SIGSEGV in a probe
-    that built and dropped many stream graphs in one process was the reason
-    to rule that order out)."""
-    st = torch.cuda.Stream(device=dev)
+    """A HIP stream of its own (pvnet_amd.streams.new_stream: torch.cuda.Stream()
+    hands out one of a pool of 32 per priority, round robin, so the bench's
+    ~40 lanes and capture streams would wrap onto each other's); like torch's
+    pooled streams it lives for the whole process."""
+    from pvnet_amd import streams
+    st = streams.new_stream(dev)
     _STREAMS.append(st)
     return st
 
 
 def new_graph():
-    """A hipGraph kept alive for the whole process, like the streams: no
-    graph is destroyed between another graph's capture and launch (a probe
-    that captured, replayed and dropped several large stream graphs in one
-    process died in a later graph's first replay, intermittently)."""
-    g = torch.cuda.CUDAGraph()
-    _GRAPHS.append(g)
-    return g
+    """A hipGraph, dropped when its last user lets go of it (round 4 kept
+    every graph for the whole process after a many-graph probe died once; the
+    same churn -- tools/extra_kernel_probe.py, 12 bench-size graphs captured,
+    replayed and dropped in turn -- runs clean: DESIGN.md "Concurrent callers")."""
+    return torch.cuda.CUDAGraph()
 
 
 def log(*a):
@@ -122,12 +120,35 @@ def parse():
     return ap.parse_args()
 
 
+def visible_gpus():
+    """GPUs this process would see, without any HIP call: the KFD topology
+    nodes with SIMDs (/sys/class/kfd/kfd/topology/nodes/*/properties), cut
+    by ROCR_/HIP_/CUDA_VISIBLE_DEVICES when set; None if sysfs is unreadable
+    (the ranks then check for themselves, setup_dist)."""
+    import glob
+    try:
+        n = 0
+        for p in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+            with open(p) as f:
+                props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+            n += int(props.get("simd_count", "0")) > 0
+    except (OSError, ValueError):
+        return None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
 def launch_ranks(args):
     """`bench.py --gpus N` (N > 1) outside torchrun: start the N ranks as child
     processes (the script again, RANK = LOCAL_RANK = r, WORLD_SIZE = N,
     MASTER_ADDR 127.0.0.1 and a free port) and wait for them.  This process
-    makes no GPU call: it only counts the devices (torch.cuda.device_count()
-    does not initialise HIP) and fails if fewer than N are visible.  Rank 0
+    makes no GPU call: it counts the devices from the KFD topology in sysfs
+    and the *_VISIBLE_DEVICES masks (visible_gpus; torch.cuda.device_count()
+    may fall back to hipGetDeviceCount, which initialises HIP before the
+    fork) and fails if fewer than N are visible.  Rank 0
     prints the JSON line.  If a rank fails, the others (this process's own
     children, by PID) are terminated.  Returns the exit code."""
     import signal
@@ -135,8 +156,8 @@ def launch_ranks(args):
     import subprocess
     n = args.gpus
     if not args.dry_run and not args.share_device:
-        have = torch.cuda.device_count()
-        if have < n:
+        have = visible_gpus()
+        if have is not None and have < n:
             log(f"bench.py --gpus {n}: only {have} GPU(s) visible")
             return 2
     with socket.socket() as so:
@@ -373,6 +394,7 @@ def dry_run(args, ws, rank):
 
 
 def main():
+    faulthandler.enable()          # a host crash names its Python frame (DESIGN.md "Concurrent callers")
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         raise SystemExit(launch_ranks(args))
@@ -581,8 +603,11 @@ def _raw_v3(rvg, seg, ver, hn, seed, work, out, dd):
     L = _lib.load()
     nbytes = L.pv_v3_workspace_size(b, h, w, c // 2, hn)
     wsb = work.get(ver.device, nbytes)
-    code = L.pv_ransac_voting_v3(ctypes.byref(d), ctypes.byref(prm), out.data_ptr(), wsb.data_ptr(), nbytes,
-                                 ctypes.byref(dd), torch.cuda.current_stream(ver.device).cuda_stream)
+    try:
+        code = L.pv_ransac_voting_v3(ctypes.byref(d), ctypes.byref(prm), out.data_ptr(), wsb.data_ptr(), nbytes,
+                                     ctypes.byref(dd), torch.cuda.current_stream(ver.device).cuda_stream)
+    finally:
+        work.done(ver.device)
     _lib.check(code, "pv_ransac_voting_v3")
     return out
 
@@ -670,13 +695,17 @@ def measure_u4(dev, reps=20):
                 e.record(s)
         torch.cuda.synchronize()
         for k, (c0, c1, v0, v1, e1) in enumerate(ev):
-            d, prm, ws, nbytes, keep = rvg._evd_common(mask, vertex, 256, 4096, 0.99, 20, 30000, 128, None, None,
-                                                        1000 + k, work)
+            d, prm, nbytes, keep, _ = rvg._evd_common(mask, vertex, 256, 4096, 0.99, 20, 30000, 128, None, None,
+                                                       1000 + k, work)
             dd = _lib.V3Diag(ev_vote_begin=v0.cuda_event, ev_vote_end=v1.cuda_event, ev_compact_end=c1.cuda_event)
+            ws = work.get(dev, nbytes)
             c0.record(s)
-            _lib.check(L.pv_estimate_voting_distribution_with_mean_diag(
-                ctypes.byref(d), ctypes.byref(prm), mean.data_ptr(), cov.data_ptr(), ws.data_ptr(), nbytes,
-                ctypes.byref(dd), s.cuda_stream), "pv_estimate_voting_distribution_with_mean_diag")
+            try:
+                _lib.check(L.pv_estimate_voting_distribution_with_mean_diag(
+                    ctypes.byref(d), ctypes.byref(prm), mean.data_ptr(), cov.data_ptr(), ws.data_ptr(), nbytes,
+                    ctypes.byref(dd), s.cuda_stream), "pv_estimate_voting_distribution_with_mean_diag")
+            finally:
+                work.done(dev)
             e1.record(s)
     torch.cuda.synchronize()
     ev = ev[3:]                                   # the first calls size the workspace and warm up

@@ -57,6 +57,18 @@ const char *pv_build_config(void); /* the build's compile-time kernel choices an
 const char *pv_error_string(int code);
 int pv_device_arch(char *buf, int len); /* writes the gcnArchName of the current device (host pointer) */
 
+/* ---- streams for concurrent callers (not in the reference: its callers are DataParallel worker
+ * threads, tools/parallel.py:183-200, each on its own device and torch's current stream) ----
+ * pv_stream_create: a new non-blocking HIP stream of its own on the current device (priority as
+ * hipStreamCreateWithPriority; 0 = default).  torch.cuda.Stream() hands out one of 32 pooled streams
+ * per priority, round robin, so the 33rd "new" stream is the 1st again: callers that need streams no
+ * one else launches on (one per in-flight lane or per launching thread) take them from here.
+ * pv_stream_capture_id: the id of the stream capture `stream` belongs to, 0 when it is not capturing
+ * (host pointer `id`); scratch owned by one captured graph is keyed by it. */
+int pv_stream_create(int32_t priority, pv_stream_t *out);
+int pv_stream_destroy(pv_stream_t stream);
+int pv_stream_capture_id(pv_stream_t stream, uint64_t *id);
+
 /* ---- drop-in kernels: the four functions of the `ransac_voting` module ---- */
 
 /* replaces generate_hypothesis (BND:20-31 -> KU:51-86).
@@ -321,6 +333,9 @@ int pv_conv3x3_ex_f16(const void *x, int32_t hin, int32_t win, int32_t stride, c
                       int32_t wd, int32_t cin, int32_t cout, int32_t dil, int32_t act, float slope, void *ws,
                       int64_t ws_bytes, pv_stream_t stream);
 int64_t pv_conv3x3_workspace_bytes(int64_t pixels, int32_t cout, int32_t ksteps);
+/* the leading bytes of that ws that hold its arrival counters (the part that must start zeroed; the
+ * rest is overwritten before it is read): a scratch made inside a graph capture zeroes only these */
+int64_t pv_conv3x3_workspace_counter_bytes(int64_t pixels, int32_t cout, int32_t ksteps);
 
 /* replaces the decoder's half-resolution step (model_repository.py:43-51,75-78: up4sto2s, torch.cat([fm,
  * x2s], 1), conv2s = 3x3 conv + BN + LeakyReLU(slope)) in one fp16 matrix-core pass: fm [n][hin][win][64]

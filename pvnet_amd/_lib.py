@@ -57,6 +57,9 @@ SIGNATURES = [
     ("pv_build_config", ctypes.c_char_p, []),
     ("pv_error_string", ctypes.c_char_p, [ctypes.c_int]),
     ("pv_device_arch", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
+    ("pv_stream_create", ctypes.c_int, [c_i32, ctypes.POINTER(c_vp)]),
+    ("pv_stream_destroy", ctypes.c_int, [c_vp]),
+    ("pv_stream_capture_id", ctypes.c_int, [c_vp, ctypes.POINTER(c_u64)]),
     ("pv_generate_hypothesis", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp]),
     ("pv_voting_for_hypothesis", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_i32, c_vp]),
     ("pv_generate_hypothesis_vp", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp]),
@@ -90,6 +93,7 @@ SIGNATURES = [
      [c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32,
       c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_f32, c_vp, c_i64, c_vp]),
     ("pv_conv3x3_workspace_bytes", c_i64, [c_i64, c_i32, c_i32]),
+    ("pv_conv3x3_workspace_counter_bytes", c_i64, [c_i64, c_i32, c_i32]),
     ("pv_decoder_conv2s_f16", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp]),
     ("pv_decoder_conv4s_f16", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp]),
     ("pv_stem_conv_f16", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp]),

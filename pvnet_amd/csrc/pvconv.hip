@@ -1619,6 +1619,11 @@ extern "C" int64_t pv_conv3x3_workspace_bytes(int64_t pixels, int32_t cout, int3
     return conv_split(pixels, cout, ksteps).bytes;
 }
 
+extern "C" int64_t pv_conv3x3_workspace_counter_bytes(int64_t pixels, int32_t cout, int32_t ksteps) {
+    if (pixels <= 0 || cout <= 0 || cout % 128 || ksteps <= 0) return 0;
+    return conv_split(pixels, cout, ksteps).tick_bytes;
+}
+
 extern "C" int pv_conv3x3_ex_f16(const void *x, int32_t hin, int32_t win, int32_t stride, const void *x2,
                                  int32_t mode2, int32_t cin2, int32_t h2, int32_t w2, int32_t s2, const void *w,
                                  const void *bias, const void *res, const void *rbias, void *out, int32_t ldo,

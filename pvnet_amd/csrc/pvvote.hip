@@ -481,9 +481,13 @@ __global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int 
     // selected pixels write consecutive records of each keypoint
     float4 *eb = pex + (int64_t)b * vn * P;
     const int64_t t = base + off;
+    // t < fg <= P whenever the counts are this call's own; the bound keeps a
+    // workspace shared by two calls in flight (a caller error) from writing
+    // past the image's records
+    const bool store = f && t < P;
     for (int v0 = 0; v0 < vn; v0 += kCompactKp) {
         if (v0 > 0) load_group(v0);
-        if (f) {
+        if (store) {
 #pragma unroll
             for (int u = 0; u < kCompactKp; ++u) {
                 if (v0 + u >= vn) break;
@@ -578,6 +582,15 @@ __device__ __forceinline__ void round_share(uint32_t total, uint32_t n, uint32_t
     };
     *lo = pos(w);
     *hi = pos(w + 1);
+}
+
+// image b's compacted pixel count, clamped to [0, P]: the vote kernels size
+// and index their work from it, so whatever the workspace holds (a caller
+// that hands one workspace to two calls in flight), every pex / hypothesis
+// index stays inside the image's P records
+__device__ __forceinline__ int tn_at(const VoteArgs &a, int b) {
+    const int n = a.tn_dev ? a.tn_dev[b] : a.tn_host;
+    return min(max(n, 0), a.P);
 }
 
 // the reference's operands of pixel t: (cx, cy, nx, ny)
@@ -1172,7 +1185,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     const int ggn = a.hgn / gpu;          // unit groups per keypoint
     // 32-bit index math (the host splits launches so that the work stays < 2^31)
     uint32_t total = 0;
-    for (int b = 0; b < a.b; ++b) total += (uint32_t)(a.vn * ggn) * (uint32_t)(a.tn_dev ? a.tn_dev[b] : a.tn_host);
+    for (int b = 0; b < a.b; ++b) total += (uint32_t)(a.vn * ggn) * (uint32_t)tn_at(a, b);
     uint32_t lo, hi;
     if (SH && a.rw[0] > 0 && nunits % 4 == 0)
         round_share(total, (uint32_t)nunits, (uint32_t)unit, a.rw, &lo, &hi);
@@ -1186,8 +1199,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     // walk the segments of [lo, hi)
     int b = 0;
     uint32_t base = 0;
-    while (lo < hi) {
-        const int n = a.tn_dev ? a.tn_dev[b] : a.tn_host;
+    while (lo < hi && b < a.b) {
+        const int n = tn_at(a, b);
         const uint32_t span = (uint32_t)(a.vn * ggn) * (uint32_t)n;
         if (lo >= base + span) { base += span; ++b; continue; }
         const uint32_t r = lo - base;
@@ -1225,7 +1238,7 @@ __global__ __launch_bounds__(256) void k_hyp_gen(VoteArgs a) {
     const int b = (int)(gid / per);
     const int r = (int)(gid - b * per);
     const int h = r / a.vn, v = r - h * a.vn;
-    const int n = a.tn_dev ? a.tn_dev[b] : a.tn_host;
+    const int n = tn_at(a, b);
     if (n > 0) a.hypv_out[((int64_t)b * a.vn + v) * a.nh + h] = item_hyp<true, true>(a, b, v, h, true, n, true);
 }
 
@@ -1325,7 +1338,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
     int32_t *corr = corr_all[wid];
     const int ggn = a.hgn / 4;
     uint32_t total = 0;
-    for (int b = 0; b < a.b; ++b) total += (uint32_t)(a.vn * ggn) * (uint32_t)(a.tn_dev ? a.tn_dev[b] : a.tn_host);
+    for (int b = 0; b < a.b; ++b) total += (uint32_t)(a.vn * ggn) * (uint32_t)tn_at(a, b);
     uint32_t lo, hi;
     if (a.rw[0] > 0 && nunits % (a.rw[3] > 0 ? 4 : 3) == 0) round_share(total, nunits, (uint32_t)unit, a.rw, &lo, &hi);
     else even_share(total, nunits, (uint32_t)unit, &lo, &hi);
@@ -1339,8 +1352,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
     constexpr float kBig = 3.0e38f;
     int b = 0;
     uint32_t base = 0;
-    while (lo < hi) {
-        const int n = a.tn_dev ? a.tn_dev[b] : a.tn_host;
+    while (lo < hi && b < a.b) {
+        const int n = tn_at(a, b);
         const uint32_t span = (uint32_t)(a.vn * ggn) * (uint32_t)n;
         if (lo >= base + span) { base += span; ++b; continue; }
         const uint32_t r0 = lo - base;
@@ -1776,7 +1789,7 @@ __global__ __launch_bounds__(kRT) void k_refine_solve(const int32_t *counts, con
                                                       float *out,
                                                       pv_v3_diag diag) {
     const int j = blockIdx.x, v = blockIdx.y, b = blockIdx.z;
-    const int n = tn[b];
+    const int n = min(max(tn[b], 0), (int)P);   // clamped like tn_at: loads stay inside the P records
     __shared__ uint64_t skey[kRW];
     __shared__ double sacc[kRW][5];
     __shared__ int slast;
@@ -2027,7 +2040,7 @@ struct MotionStage {
 __global__ __launch_bounds__(256) void k_point_conf(const float *pts, const float4 *pex, const int32_t *tn, int64_t P,
                                                     int vn, float thr, int32_t *confc, float *conf) {
     const int j = blockIdx.x, v = blockIdx.y, b = blockIdx.z;
-    const int n = tn[b];
+    const int n = min(max(tn[b], 0), (int)P);   // clamped like tn_at: loads stay inside the P records
     __shared__ int sh[8];
     const float px = pts[((int64_t)b * vn + v) * 2], py = pts[((int64_t)b * vn + v) * 2 + 1];
     const float4 *eb = pex + ((int64_t)b * vn + v) * P;
@@ -3324,6 +3337,30 @@ int pv_device_arch(char *buf, int len) {
         strncpy(buf, prop.gcnArchName, (size_t)len - 1);
         buf[len - 1] = 0;
     }
+    return PV_OK;
+}
+
+int pv_stream_create(int32_t priority, pv_stream_t *out) {
+    if (!out) return PV_EINVAL;
+    hipStream_t s = nullptr;
+    const hipError_t e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority);
+    if (e != hipSuccess) return rc(e);
+    *out = (pv_stream_t)s;
+    return PV_OK;
+}
+
+int pv_stream_destroy(pv_stream_t stream) {
+    if (!stream) return PV_EINVAL;
+    return rc(hipStreamDestroy((hipStream_t)stream));
+}
+
+int pv_stream_capture_id(pv_stream_t stream, uint64_t *id) {
+    if (!id) return PV_EINVAL;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    unsigned long long cid = 0;
+    const hipError_t e = hipStreamGetCaptureInfo((hipStream_t)stream, &st, &cid);
+    if (e != hipSuccess) return rc(e);
+    *id = st == hipStreamCaptureStatusActive ? (uint64_t)cid : 0;
     return PV_OK;
 }
 

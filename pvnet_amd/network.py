@@ -402,42 +402,61 @@ def conv3x3(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, dil: int, act:
     return out
 
 
-_CONV_WS: dict = {}
-_CONV_WS_LOCK = threading.Lock()     # per-GPU threads (DataParallel-style callers) share the table
+_CONV_WS: dict = {}         # eager calls: (device, stream) -> [buffers]
+_CAPTURE_WS: dict = {}      # inside a capture: (device, stream, capture id) -> the graph's own buffer
+_CONV_WS_LOCK = threading.Lock()     # per-GPU threads (DataParallel-style callers) share the tables
 
 
 def clear_conv_workspaces() -> None:
-    """Drop every split-K scratch buffer (no captured graph that used one may
-    be replayed afterwards)."""
+    """Drop every eager split-K scratch buffer (no captured graph that used
+    one may be replayed afterwards; graph-owned scratch lives in the graphs'
+    own memory pools)."""
     with _CONV_WS_LOCK:
         _CONV_WS.clear()
+        _CAPTURE_WS.clear()
 
 CONV_SPLIT = True          # the split-K last round (A/B hook for tools/backbone_ab2.py; no environment switch)
 
 
 def _conv_workspace(x: torch.Tensor, pixels: int, cout: int, ksteps: int):
     """The split-K scratch of pv_conv3x3_ex_f16 (its last partial round of
-    tiles): one buffer per (device, stream), since calls on one stream run in
-    order; grown to the largest need and kept, so a captured graph keeps
-    using the buffer it captured.  Its arrival counters must start at zero,
-    so buffers are only made (zero-filled) outside a stream capture: inside
-    one, a call with no large enough buffer runs without split-K (ws NULL)
-    rather than take memory whose zero fill would only run at replay.  A
-    process that keeps creating streams should call
-    :func:`clear_conv_workspaces` once their graphs are gone.
+    tiles; arrival counters that must start at zero, then f32 partials).
+
+    Eager calls: one buffer per (device, stream), since calls on one stream
+    run in order; zero-filled when made, grown to the largest need and kept
+    (every call leaves its counters at zero again).
+
+    Inside a graph capture: a buffer of the capture's own, per (stream,
+    capture id) -- taken from the graph's private memory pool, its counters
+    zeroed by a fill captured before the capture's first convolution on that
+    stream (so every replay starts from zero).  Graphs captured on one shared
+    stream therefore never share counters and can replay concurrently.
     (pointer, bytes) or (None, 0)."""
     from pvnet_amd import _lib
-    need = int(_lib.load().pv_conv3x3_workspace_bytes(pixels, cout, ksteps))
+    from pvnet_amd import streams
+    L = _lib.load()
+    need = int(L.pv_conv3x3_workspace_bytes(pixels, cout, ksteps))
     if need <= 0 or not CONV_SPLIT:
         return None, 0
-    key = (x.device, torch.cuda.current_stream(x.device).cuda_stream)
-    capturing = torch.cuda.is_current_stream_capturing()
+    stream = torch.cuda.current_stream(x.device)
+    if torch.cuda.is_current_stream_capturing():
+        cid = streams.capture_id(stream)
+        key = (x.device, stream.cuda_stream, cid)
+        with _CONV_WS_LOCK:
+            for k in [k for k in _CAPTURE_WS if k[2] != cid]:
+                del _CAPTURE_WS[k]      # an earlier capture's: its graph's pool keeps the memory
+            buf = _CAPTURE_WS.get(key)
+            if buf is None or buf.numel() < need:
+                buf = torch.empty(need, dtype=torch.uint8, device=x.device)
+                nc = int(L.pv_conv3x3_workspace_counter_bytes(pixels, cout, ksteps))
+                buf[:nc].zero_()        # captured: runs at every replay, before this call's kernel
+                _CAPTURE_WS[key] = buf
+            return buf.data_ptr(), buf.numel()
+    key = (x.device, stream.cuda_stream)
     with _CONV_WS_LOCK:
         bufs = _CONV_WS.setdefault(key, [])
         if not bufs or bufs[-1].numel() < need:
-            if capturing:
-                return None, 0
-            # a smaller buffer is kept alive too: a graph captured with it still uses it
+            # a smaller buffer is kept alive too: a graph captured with it before still uses it
             bufs.append(torch.zeros(need, dtype=torch.uint8, device=x.device))   # zeroed once (pvvote.h)
         return bufs[-1].data_ptr(), bufs[-1].numel()
 

@@ -29,6 +29,7 @@ cannot be reproduced anyway); fp32 least-squares sums are accumulated in fp64
 from __future__ import annotations
 
 import ctypes
+import threading
 
 import numpy as np
 import torch
@@ -56,36 +57,81 @@ class VotingWorkspace:
     (needed for hipGraph capture: no allocation inside the captured region).
 
     A pipeline call zeroes and rewrites its workspace, so two calls in flight
-    on different streams must not share one: an explicit workspace belongs to
-    one stream at a time (pass one per stream, as ``bench.py`` does), and the
-    default workspace (used when ``_workspace`` is omitted) keeps one buffer
-    per (device, stream).  A buffer that grows is released with
-    ``record_stream`` for every stream that used it, so the caching allocator
-    never hands it out while a kernel can still touch it.  Growing inside a
-    graph capture raises: warm the workspace up (one eager call of the same
-    shape) before capturing."""
+    on different streams must not share one.
+
+    * An explicit workspace (``_workspace=``, ``per_stream=False``) holds one
+      call at a time: an eager call on a stream other than the one its
+      previous call ran on raises ``RuntimeError`` if that call is still in
+      flight (an event recorded after each call), so two threads handing one
+      workspace to their own streams get an error, not a race.  Inside a
+      graph capture there is no check (the call runs when the graph is
+      replayed): a workspace captured into a graph belongs to that graph, and
+      two graphs that may replay at the same time need one each.  Growing
+      inside a capture raises: warm the workspace up (one eager call of the
+      same shape) before capturing.
+    * The default workspace (used when ``_workspace`` is omitted,
+      ``per_stream=True``) keeps one buffer per (device, stream) for eager
+      calls, and inside a capture takes a fresh buffer from the capturing
+      graph's private memory pool for every call: each captured graph owns
+      its scratch, so graphs captured on one shared stream (torch.cuda.graph
+      without ``stream=``) can replay concurrently.
+
+    A buffer that grows is released with ``record_stream`` for every stream
+    that used it, so the caching allocator never hands it out while a kernel
+    can still touch it.  Thread-safe (one lock per workspace)."""
 
     def __init__(self, per_stream: bool = False):
         self._buf = {}
         self._streams = {}
         self._per_stream = per_stream
+        self._lock = threading.Lock()
+        self._owner = {}       # explicit: key -> [stream handle of the last call, busy, event after it]
+
+    def _key(self, device, stream):
+        return (str(device), stream.cuda_stream) if self._per_stream else (str(device),)
 
     def get(self, device, nbytes: int) -> torch.Tensor:
         stream = torch.cuda.current_stream(device)
-        key = (str(device), stream.cuda_stream) if self._per_stream else (str(device),)
-        buf = self._buf.get(key)
-        if buf is None or buf.numel() < nbytes:
-            if torch.cuda.is_current_stream_capturing():
-                raise RuntimeError("VotingWorkspace would allocate during graph capture: make one eager call of "
-                                   "the same shape with this workspace (_workspace=...) before capturing")
-            if buf is not None:
-                for st in self._streams.get(key, ()):
-                    buf.record_stream(st)
-            buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
-            self._buf[key] = buf
-            self._streams[key] = set()
-        self._streams[key].add(stream)
-        return buf
+        capturing = torch.cuda.is_current_stream_capturing()
+        if capturing and self._per_stream:
+            # the default workspace inside a capture: the graph's own (private pool)
+            return torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+        key = self._key(device, stream)
+        with self._lock:
+            if not self._per_stream and not capturing:
+                own = self._owner.setdefault(key, [stream.cuda_stream, False, None])
+                if own[0] != stream.cuda_stream and (own[1] or (own[2] is not None and not own[2].query())):
+                    raise RuntimeError("VotingWorkspace is in use by a call in flight on another stream: give each "
+                                       "stream (each launching thread) its own workspace")
+                own[0], own[1] = stream.cuda_stream, True
+            buf = self._buf.get(key)
+            if buf is None or buf.numel() < nbytes:
+                if capturing:
+                    raise RuntimeError("VotingWorkspace would allocate during graph capture: make one eager call of "
+                                       "the same shape with this workspace (_workspace=...) before capturing")
+                if buf is not None:
+                    for st in self._streams.get(key, ()):
+                        buf.record_stream(st)
+                buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+                self._buf[key] = buf
+                self._streams[key] = set()
+            self._streams[key].add(stream)
+            return buf
+
+    def done(self, device) -> None:
+        """After the library call that used get()'s buffer was queued (or
+        failed): an event on its stream marks when the workspace is free."""
+        if self._per_stream or torch.cuda.is_current_stream_capturing():
+            return
+        stream = torch.cuda.current_stream(device)
+        with self._lock:
+            own = self._owner.get(self._key(device, stream))
+            if own is None or own[0] != stream.cuda_stream:
+                return
+            if own[2] is None:
+                own[2] = torch.cuda.Event()
+            own[2].record(stream)
+            own[1] = False
 
 
 _default_ws = VotingWorkspace(per_stream=True)
@@ -164,7 +210,7 @@ def _v3(d, mask, vertex, round_hyp_num, inlier_thresh, confidence, max_iter, min
     prm = _params(round_hyp_num, inlier_thresh, confidence, max_iter, min_num, max_num, _seed, idxs, keep)
     L = _lib.load()
     nbytes = L.pv_v3_workspace_size(b, h, w, vn, round_hyp_num)
-    ws = (_workspace or _default_ws).get(dev, nbytes)
+    work = _workspace or _default_ws
     if out is None:
         out = torch.empty((b, vn, 2), dtype=torch.float32, device=dev)
     diag = None
@@ -179,18 +225,21 @@ def _v3(d, mask, vertex, round_hyp_num, inlier_thresh, confidence, max_iter, min
                   ata=torch.empty((b, vn, 2, 2), dtype=torch.float32, device=dev),
                   atb=torch.empty((b, vn, 2), dtype=torch.float32, device=dev))
         diag = _lib.V3Diag(**{k: v.data_ptr() for k, v in dt.items()})
-    conf = None
+    conf = None if conf_thresh is None else torch.empty((b, vn), dtype=torch.float32, device=dev)
+    ws = work.get(dev, nbytes)
     with torch.cuda.device(dev):
-        if conf_thresh is None:
-            code = L.pv_ransac_voting_v3(ctypes.byref(d), ctypes.byref(prm), out.data_ptr(), ws.data_ptr(), nbytes,
-                                         ctypes.byref(diag) if diag is not None else None,
-                                         torch.cuda.current_stream(dev).cuda_stream)
-        else:
-            conf = torch.empty((b, vn), dtype=torch.float32, device=dev)
-            code = L.pv_ransac_voting_v5(ctypes.byref(d), ctypes.byref(prm), float(conf_thresh), out.data_ptr(),
-                                         conf.data_ptr(), ws.data_ptr(), nbytes,
-                                         ctypes.byref(diag) if diag is not None else None,
-                                         torch.cuda.current_stream(dev).cuda_stream)
+        try:
+            if conf_thresh is None:
+                code = L.pv_ransac_voting_v3(ctypes.byref(d), ctypes.byref(prm), out.data_ptr(), ws.data_ptr(), nbytes,
+                                             ctypes.byref(diag) if diag is not None else None,
+                                             torch.cuda.current_stream(dev).cuda_stream)
+            else:
+                code = L.pv_ransac_voting_v5(ctypes.byref(d), ctypes.byref(prm), float(conf_thresh), out.data_ptr(),
+                                             conf.data_ptr(), ws.data_ptr(), nbytes,
+                                             ctypes.byref(diag) if diag is not None else None,
+                                             torch.cuda.current_stream(dev).cuda_stream)
+        finally:
+            work.done(dev)
     _lib.check(code, "ransac_voting_layer_v3" if conf_thresh is None else "ransac_voting_layer_v5")
     if _diag is not None:
         _diag.update(dt)
@@ -263,25 +312,28 @@ def _evd_common(mask, vertex, round_hyp_num, min_hyp_num, inlier_thresh, min_num
                   min_hyp_num=min_hyp_num, topk=topk)
     L = _lib.load()
     nbytes = L.pv_v3_workspace_size(d.b, d.H, d.W, d.vn, nh)
-    ws = (_workspace or _default_ws).get(dev, nbytes)
-    return d, prm, ws, nbytes, (idxs, keep)
+    return d, prm, nbytes, (idxs, keep), _workspace or _default_ws
 
 
 def estimate_voting_distribution_with_mean(mask, vertex, mean, round_hyp_num=256, min_hyp_num=4096, topk=128,
                                            inlier_thresh=0.99, min_num=20, max_num=30000, output_hyp=False, *,
                                            _idxs=None, _keep=None, _seed=None, _workspace=None):
     """RV:333-406 -> (mean, cov [b,vn,2,2]).  ``_idxs`` is [b, rounds*round_hyp_num, vn, 2]."""
-    d, prm, ws, nbytes, keepalive = _evd_common(mask, vertex, round_hyp_num, min_hyp_num, inlier_thresh, min_num,
-                                                max_num, topk, _idxs, _keep, _seed, _workspace)
+    d, prm, nbytes, keepalive, work = _evd_common(mask, vertex, round_hyp_num, min_hyp_num, inlier_thresh, min_num,
+                                                  max_num, topk, _idxs, _keep, _seed, _workspace)
     dev = vertex.device
     mean_c = mean.to(device=dev, dtype=torch.float32).contiguous()
     if tuple(mean_c.shape) != (d.b, d.vn, 2):
         raise RuntimeError("mean must be [b,vn,2]")
     cov = torch.empty((d.b, d.vn, 2, 2), dtype=torch.float32, device=dev)
+    ws = work.get(dev, nbytes)
     with torch.cuda.device(dev):
-        code = _lib.load().pv_estimate_voting_distribution_with_mean(
-            ctypes.byref(d), ctypes.byref(prm), mean_c.data_ptr(), cov.data_ptr(), ws.data_ptr(), nbytes,
-            torch.cuda.current_stream(dev).cuda_stream)
+        try:
+            code = _lib.load().pv_estimate_voting_distribution_with_mean(
+                ctypes.byref(d), ctypes.byref(prm), mean_c.data_ptr(), cov.data_ptr(), ws.data_ptr(), nbytes,
+                torch.cuda.current_stream(dev).cuda_stream)
+        finally:
+            work.done(dev)
     _lib.check(code, "estimate_voting_distribution_with_mean")
     return mean, cov
 
@@ -289,15 +341,19 @@ def estimate_voting_distribution_with_mean(mask, vertex, mean, round_hyp_num=256
 def estimate_voting_distribution(mask, vertex, round_hyp_num=256, min_hyp_num=4096, topk=128, inlier_thresh=0.99,
                                  min_num=5, max_num=30000, *, _idxs=None, _keep=None, _seed=None, _workspace=None):
     """RV:263-331 -> (mean [b,vn,2], cov [b,vn,2,2]); topk ties lowest index first."""
-    d, prm, ws, nbytes, keepalive = _evd_common(mask, vertex, round_hyp_num, min_hyp_num, inlier_thresh, min_num,
-                                                max_num, topk, _idxs, _keep, _seed, _workspace)
+    d, prm, nbytes, keepalive, work = _evd_common(mask, vertex, round_hyp_num, min_hyp_num, inlier_thresh, min_num,
+                                                  max_num, topk, _idxs, _keep, _seed, _workspace)
     dev = vertex.device
     mean = torch.empty((d.b, d.vn, 2), dtype=torch.float32, device=dev)
     cov = torch.empty((d.b, d.vn, 2, 2), dtype=torch.float32, device=dev)
+    ws = work.get(dev, nbytes)
     with torch.cuda.device(dev):
-        code = _lib.load().pv_estimate_voting_distribution(
-            ctypes.byref(d), ctypes.byref(prm), mean.data_ptr(), cov.data_ptr(), ws.data_ptr(), nbytes,
-            torch.cuda.current_stream(dev).cuda_stream)
+        try:
+            code = _lib.load().pv_estimate_voting_distribution(
+                ctypes.byref(d), ctypes.byref(prm), mean.data_ptr(), cov.data_ptr(), ws.data_ptr(), nbytes,
+                torch.cuda.current_stream(dev).cuda_stream)
+        finally:
+            work.done(dev)
     _lib.check(code, "estimate_voting_distribution")
     return mean, cov
 

@@ -962,12 +962,14 @@ def test_conv3x3_ex_eligibility():
 @pytest.mark.gpu
 def test_conv_split_scratch_capture_without_warmup(device):
     """The split-K scratch of pv_conv3x3_ex_f16 and graph capture (advisor,
-    round 3): capture a convolution whose last round of tiles is split, on a
-    fresh stream with no warm-up, then run the same call eagerly on that stream
-    BEFORE any replay, then replay.  The capture runs without split-K (no
-    buffer is made inside it), the eager calls make and zero a buffer outside
-    it; every output is within the fp16 bound of the f64 convolution, the two
-    eager calls are bit-equal, and the replay equals the captured form."""
+    rounds 3 and 4): capture a convolution whose last round of tiles is
+    split, on a fresh stream with no warm-up, then run the same call eagerly
+    on that stream BEFORE any replay, then replay.  The capture takes a
+    scratch of its own from the graph's pool and captures the fill of its
+    counters; the eager calls make and zero a buffer outside it.  Every
+    output is within the fp16 bound of the f64 convolution, and the replay
+    and both eager calls are bit-equal (the same split, summed in part
+    order)."""
     from pvnet_amd.network import clear_conv_workspaces, conv3x3, conv3x3_weight
     F = torch.nn.functional
     g = torch.Generator().manual_seed(404)
@@ -992,6 +994,7 @@ def test_conv_split_scratch_capture_without_warmup(device):
     graph.replay()
     torch.cuda.synchronize()
     assert torch.equal(e1, e2)
+    assert torch.equal(got_g, e1)
     with torch.no_grad():
         c64 = B.conv64(x, conv.weight, padding=d, dilation=d)
         e = B.round_step(c64, B.acc_bound(x, conv.weight, 9 * cin, padding=d, dilation=d))

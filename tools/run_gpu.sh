@@ -15,6 +15,8 @@ step() {  # step <name> <seconds> <cmd...>
 }
 for s in "$@"; do
   case $s in
+    threads) step gpu_threads 300 python -u -m pytest tests/test_gpu_threads.py -x -v --timeout 200 --timeout-method thread ;;
+    rtp) step rtp 300 python3 tools/replay_threads_probe.py ;;
     tests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     testsall) step gpu_tests 900 python -m pytest tests -m gpu -q ;;
     lat) step lat 120 python3 tools/lat_trace.py 20 &&
