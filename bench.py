@@ -110,6 +110,7 @@ def parse():
     ap.add_argument("--skip-u1", action="store_true")
     ap.add_argument("--skip-config3", action="store_true", help="skip the configs[3] and configs[4] stream legs")
     ap.add_argument("--skip-u4", action="store_true", help="skip the U4 (EVD with mean) timing")
+    ap.add_argument("--skip-batched", action="store_true", help="skip the stream_batched4 leg")
     ap.add_argument("--share-device", action="store_true",
                     help="test hook for a one-GPU box: every rank on cuda:0 over gloo (RCCL refuses two ranks on one "
                          "device), the real GPU path otherwise -- checks the N > 1 code, not its speed")
@@ -228,13 +229,20 @@ def field_seed(i, ws, nfields):
 
 
 def make_fields(rank, ws, nfields, dev):
-    """The rank's resident fields (network layout, f32), seed 1234 + rank + ws*f."""
+    """The rank's resident fields (network layout, f32), seed 1234 + rank + ws*f:
+    views [1, ...] of one [nfields, ...] tensor each (so consecutive fields
+    are also a batch: the stream_batched leg)."""
     from pvnet_amd import synth
     segs, vers, kps = [], [], []
     for f in range(nfields):
         fd = synth.synthetic_field(1234 + rank + ws * f)
-        segs.append(torch.from_numpy(fd["seg"]).to(dev))
-        vers.append(torch.from_numpy(fd["vertex"]).to(dev))
+        if f == 0:
+            seg_all = torch.empty((nfields,) + fd["seg"].shape[1:], dtype=torch.float32, device=dev)
+            ver_all = torch.empty((nfields,) + fd["vertex"].shape[1:], dtype=torch.float32, device=dev)
+        seg_all[f].copy_(torch.from_numpy(fd["seg"][0]))
+        ver_all[f].copy_(torch.from_numpy(fd["vertex"][0]))
+        segs.append(seg_all[f:f + 1])
+        vers.append(ver_all[f:f + 1])
         kps.append(fd["keypoints"])
     return segs, vers, np.stack(kps), int(fd["tn"])
 
@@ -255,20 +263,23 @@ def make_stream_fields(rank, ws, nfields, dev):
     return segs, vers, np.stack(kps), np.array(tns), kinds
 
 
-def graph_stream(args, ws, rank, dev, steps, seed_base, vote, parts, per_step=None, lanes_state=None):
+def graph_stream(args, ws, rank, dev, steps, seed_base, vote, parts, per_step=None, lanes_state=None,
+                 frames_per_call=1, stats=None):
     """The timed stream core: this rank's share (pvnet_amd.distributed.shard)
-    of ws * steps * M images; one step = one hipGraph replay of M calls of
-    ``vote(j, seed, lane, outs)`` (slot j writes row j of each per-step output
-    in ``outs``), --inflight of them at a time on their own streams; one
-    gather of every image's result at the end of the timed region.
-    ``parts`` = [(shape, dtype)] of one image's result.  Returns (elapsed s
-    (max over ranks), local results [steps*M, ...] per part, gathered
-    results per part (stream order), the capture stream)."""
+    of ws * steps * M images; one step = one hipGraph replay of M /
+    frames_per_call calls of ``vote(j, seed, lane, outs)`` (the call at frame
+    j writes rows j .. j + frames_per_call - 1 of each per-step output in
+    ``outs``), --inflight of them at a time on their own streams; one gather
+    of every image's result at the end of the timed region.  ``parts`` =
+    [(shape, dtype)] of one image's result.  ``stats`` (a dict) receives the
+    host seconds spent inside the timed graph.replay() calls.  Returns
+    (elapsed s (max over ranks), local results [steps*M, ...] per part,
+    gathered results per part (stream order), the capture stream)."""
     from pvnet_amd import distributed as D
     M, K = per_step or args.per_step, steps
     n_images = ws * K * M                          # the whole stream, sharded round-robin (SURVEY 8(e))
     mine = D.shard(n_images, rank, ws)             # this rank's images, in stream order
-    assert len(mine) == K * M
+    assert len(mine) == K * M and M % frames_per_call == 0
     NL = max(1, args.inflight)
     lanes = [new_stream(dev) for _ in range(NL)]
     outs = [torch.zeros((M,) + tuple(sh), dtype=dt, device=dev) for sh, dt in parts]
@@ -278,9 +289,9 @@ def graph_stream(args, ws, rank, dev, steps, seed_base, vote, parts, per_step=No
     def step_body(seed0):
         for ln in lanes:
             ln.wait_stream(torch.cuda.current_stream())
-        for j in range(M):
-            with torch.cuda.stream(lanes[j % NL]):
-                vote(j, seed0 + 17 * j, j % NL, outs)
+        for c, j in enumerate(range(0, M, frames_per_call)):
+            with torch.cuda.stream(lanes[c % NL]):
+                vote(j, seed0 + 17 * j, c % NL, outs)
         for ln in lanes:
             torch.cuda.current_stream().wait_stream(ln)
 
@@ -299,10 +310,13 @@ def graph_stream(args, ws, rank, dev, steps, seed_base, vote, parts, per_step=No
     if ws > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    host = 0.0
     t0 = time.perf_counter()
     with torch.cuda.stream(s):
         for k in range(K):
+            h0 = time.perf_counter()
             graph.replay()
+            host += time.perf_counter() - h0
             for loc, o in zip(local, outs):
                 loc[k * M:(k + 1) * M].copy_(o)
         # the stream's one exchange: every image's result to every rank, in
@@ -322,23 +336,39 @@ def graph_stream(args, ws, rank, dev, steps, seed_base, vote, parts, per_step=No
         mine_t = torch.tensor(mine, device=dev)
         for a_, l_ in zip(allr, local):
             assert torch.equal(a_[mine_t], l_), "gathered stream order differs from the shard"
+    if stats is not None:
+        stats["host_replay_s"] = host
     return elapsed, local, allr, s
 
 
-def run_stream(args, ws, rank, dev, segs, vers, steps, seed_base):
+def run_stream(args, ws, rank, dev, segs, vers, steps, seed_base, frames_per_call=1, stats=None):
     """The v3 stream: ransac_voting_layer_v3 on seg_pred/vertex_pred of
-    resident field j % len(segs) per slot, its own workspace per lane.
+    resident field j % len(segs) per slot, its own workspace per lane.  With
+    frames_per_call f > 1 one call votes f consecutive resident fields as a
+    batch (segs / vers must then be consecutive views of one tensor).
     Returns (elapsed s (max over ranks), local keypoints [steps*M, 9, 2],
     lanes' workspaces, the capture stream, gathered keypoints)."""
     from pvnet_amd import ransac_voting_gpu as rvg
     NF = len(segs)
+    f = frames_per_call
     works = [rvg.VotingWorkspace() for _ in range(max(1, args.inflight))]
+    if f > 1:
+        assert NF % f == 0
+        seg_all = segs[0].as_strided((NF,) + tuple(segs[0].shape[1:]), segs[0].stride())
+        ver_all = vers[0].as_strided((NF,) + tuple(vers[0].shape[1:]), vers[0].stride())
+        assert all(segs[i].data_ptr() == seg_all[i].data_ptr() and vers[i].data_ptr() == ver_all[i].data_ptr()
+                   for i in range(NF)), "batched frames must be consecutive views of one tensor"
 
     def vote(j, seed, lane, outs):
-        rvg.ransac_voting_layer_v3_from_network(segs[j % NF], vers[j % NF], args.hn, _seed=seed,
-                                               _workspace=works[lane], out=outs[0][j:j + 1])
+        if f == 1:
+            rvg.ransac_voting_layer_v3_from_network(segs[j % NF], vers[j % NF], args.hn, _seed=seed,
+                                                   _workspace=works[lane], out=outs[0][j:j + 1])
+        else:
+            i = j % NF
+            rvg.ransac_voting_layer_v3_from_network(seg_all[i:i + f], ver_all[i:i + f], args.hn, _seed=seed,
+                                                   _workspace=works[lane], out=outs[0][j:j + f])
     elapsed, local, allr, s = graph_stream(args, ws, rank, dev, steps, seed_base, vote,
-                                           [((VN, 2), torch.float32)])
+                                           [((VN, 2), torch.float32)], frames_per_call=f, stats=stats)
     return elapsed, local[0], works, s, allr[0]
 
 
@@ -408,7 +438,8 @@ def main():
     segs, vers, kps, tn = make_fields(rank, ws, NF, dev)
     # local image j (stream image rank + ws * j) votes field j % NF: field_seed == 1234 + rank + ws * (j % NF)
     assert all(field_seed(rank + ws * j, ws, NF) == 1234 + rank + ws * (j % NF) for j in range(4 * NF))
-    elapsed, local, works, s, allkp = run_stream(args, ws, rank, dev, segs, vers, K, 0)
+    hs = {}
+    elapsed, local, works, s, allkp = run_stream(args, ws, rank, dev, segs, vers, K, 0, stats=hs)
     # every gathered image against its field's generating keypoints: a result
     # in the wrong stream slot would be tens of pixels off
     order_err = stream_order_error(allkp, ws, NF)
@@ -426,6 +457,13 @@ def main():
         err = float(e.item())
     if err > 5.0:
         raise SystemExit(f"keypoint error {err} px > 5 on the synthetic fields (tn={tn})")
+
+    # the same stream with 4 consecutive resident frames per call (one batched
+    # v3 call: 5 kernel nodes per 4 frames instead of per frame): separates
+    # the host's per-node graph submission from the GPU's work per frame
+    sb = None
+    if not args.skip_batched:
+        sb = stream_batched(args, ws, rank, dev, segs, vers, kps, 4)
 
     # configs[3]: the Occlusion-LINEMOD-like stream (mixed masks), the same
     # sharding and gather, fewer steps
@@ -452,12 +490,31 @@ def main():
     torch.cuda.synchronize()
     latency_ms = (time.perf_counter() - t1) / NLAT * 1e3
     res = dict(elapsed=elapsed, vote_ms=vote_ms, compact_ms=compact_ms, tn=tn, latency_ms=latency_ms,
-               n_images=n_images, config3=c3, config4=c4, order_err=order_err)
+               n_images=n_images, config3=c3, config4=c4, order_err=order_err, batched=sb,
+               host_ms_per_replay=hs["host_replay_s"] / K * 1e3)
     if rank == 0:
         report(args, ws, res, err, dev)
     if ws > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def stream_batched(args, ws, rank, dev, segs, vers, kps, f):
+    """stream_batched<f>: the headline stream's frames, sharding, lanes and
+    gather, but each lane call votes f consecutive resident frames as one
+    batch (RV:531's per-image loop is batched in the reference's pipeline
+    too): 5 kernel nodes per f frames.  Not the headline (batch-1 frames)."""
+    K, M, NF = args.steps, args.per_step, len(segs)
+    hs = {}
+    elapsed, local, _, _, _ = run_stream(args, ws, rank, dev, segs, vers, K, 77_000, frames_per_call=f, stats=hs)
+    n = ws * K * M
+    err = float(np.abs(local.cpu().numpy() - kps[np.arange(K * M) % NF]).max())
+    return dict(images_per_s=round(n / elapsed, 1), ms_per_step=round(elapsed / K * 1e3, 4), steps=K,
+                frames_per_call=f, per_gpu_batch_per_step=M, kernel_nodes_per_frame=5.0 / f,
+                host_ms_per_replay=round(hs["host_replay_s"] / K * 1e3, 4), max_kp_err_px=round(err, 4),
+                note="the headline stream (same fields, 8 lanes, one graph replay per %d frames) with %d consecutive "
+                     "frames per ransac_voting_layer_v3 call; host_ms_per_replay = host time inside "
+                     "graph.replay() (the runtime's submission of the replay's kernel nodes)" % (M, f))
 
 
 def stream_config3(args, ws, rank, dev, steps=8):
@@ -1163,8 +1220,11 @@ def report(args, ws, res, final_err, dev):
         "stream_order_max_err_px": round(res["order_err"], 5),
         "stream_order_ok": res["order_err"] <= 5.0,
         "latency_ms_per_image": round(res["latency_ms"], 5),
+        "host_ms_per_replay": round(res["host_ms_per_replay"], 4),
         "library": library_config(),
     }
+    if res.get("batched") is not None:
+        line["stream_batched4"] = res["batched"]
     if res.get("config3") is not None:
         line["stream_config3"] = res["config3"]
     if res.get("config4") is not None:
