@@ -334,7 +334,8 @@ int pv_conv3x3_ex_f16(const void *x, int32_t hin, int32_t win, int32_t stride, c
                       int64_t ws_bytes, pv_stream_t stream);
 int64_t pv_conv3x3_workspace_bytes(int64_t pixels, int32_t cout, int32_t ksteps);
 /* the leading bytes of that ws that hold its arrival counters (the part that must start zeroed; the
- * rest is overwritten before it is read): a scratch made inside a graph capture zeroes only these */
+ * rest is overwritten before it is read): a scratch made inside a graph capture zeroes only these.
+ * The same 4 KiB for every shape that splits, so one ws serves calls of any shapes in turn. */
 int64_t pv_conv3x3_workspace_counter_bytes(int64_t pixels, int32_t cout, int32_t ksteps);
 
 /* replaces the decoder's half-resolution step (model_repository.py:43-51,75-78: up4sto2s, torch.cat([fm,

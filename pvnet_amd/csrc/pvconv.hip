@@ -36,10 +36,18 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/pvvote.h"
 
 #ifndef PVC_PT_MAJOR
 #define PVC_PT_MAJOR 1      // k_conv3x3 tile order within an XCD's range: 1 pixel tile major (5.41-5.45 -> 5.29 ms backbone), 0 cout tile major
+#endif
+#ifndef PVC_DEC_V1
+#define PVC_DEC_V1 0        // 1: the decoder steps on the round-4 kernels (k_dec_conv2s / 4s: halo build and MFMAs in sequence; A/B)
+#endif
+#ifndef PVC_DEC_AHEAD
+#define PVC_DEC_AHEAD 3     // k_dec_conv consumers: fragment reads this many k-steps ahead of their MFMAs
 #endif
 #ifndef PVC_L1_AHEAD
 #define PVC_L1_AHEAD 2      // halo kernels (k_conv64, k_dec_conv2s / 4s): fragment reads this many k-steps ahead of their MFMAs
@@ -120,7 +128,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t image_rsrc(const void *base, i
 // is built, so they land during this tile's convolution and nothing holds
 // registers for them (round 4; before: loads into 15 VGPRs and an LDS store
 // phase, which kept the kernel at 2 blocks per CU).
-__device__ __forceinline__ void fetch(const TailArgs &a, int tile, _Float16 *patch, uint32_t *imgs) {
+[[maybe_unused]] __device__ __forceinline__ void fetch(const TailArgs &a, int tile, _Float16 *patch, uint32_t *imgs) {
     int b, y0, x0, ly0, lx0;
     tile_coords(a, tile, b, y0, x0, ly0, lx0);
     const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
@@ -219,6 +227,12 @@ __device__ __forceinline__ void halo_blend(const TailArgs &a, const _Float16 *pa
     *(h8 *)(halo + hy * (kHC * kCP) + (c >> 2) * kCP + 8 * (c & 3)) = v;
 }
 
+#ifndef PVT_V1
+#define PVT_V1 1             // 1: k_decoder_tail (3 blocks per CU); 0: k_decoder_tail2, warp-specialised (A/B: measured slower)
+#endif
+#ifndef PVT_AHEAD
+#define PVT_AHEAD 3          // k_decoder_tail2 consumers: B fragments this many k-steps ahead
+#endif
 #ifndef PVT_WPE
 #define PVT_WPE 3            // waves per SIMD the tail's registers are sized for (blocks of 4 waves per CU)
 #endif
@@ -226,6 +240,7 @@ __device__ __forceinline__ void halo_blend(const TailArgs &a, const _Float16 *pa
 #define PVT_WREG 12          // k-steps whose weights stay in registers (cout <= 32; 2 fewer above); the rest in LDS
 #endif
 
+#if PVT_V1
 template <int COUT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVT_WPE, PVT_WPE))) void k_decoder_tail(TailArgs a) {
     constexpr int MT = (COUT + 31) / 32;
@@ -383,9 +398,199 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVT_WPE, PV
     }
 }
 
+#endif  // PVT_V1
+
 #ifdef PVT_TRACE
 unsigned long long *g_tail_trace = nullptr;
 #endif
+
+// The tail, warp-specialised (round 5): one block of 8 waves per CU, waves
+// 0-3 consumers (two output rows each: 46 MFMAs per tile, A fragments -- all
+// 23 k-steps of the 3x3 weights -- in registers for the launch, the 1x1
+// head's too), waves 4-7 producers: per tile they LDS-DMA the fm patch and
+// image rows of the tile two ahead and build the halo of the next tile into
+// the other of two halo buffers (k_decoder_tail's blend, make_geo's task
+// split: the same values), so the halo build runs beside the MFMAs instead
+// of between them.  One barrier per tile.  LDS: 2 halos (54.4 KB), 2 patch +
+// image buffers (21 KB).
+template <int COUT>
+__global__ __launch_bounds__(512) void k_decoder_tail2(TailArgs a) {
+    constexpr int MT = (COUT + 31) / 32;
+    __shared__ alignas(16) _Float16 halo2[2][kHaloPx * kCP];
+    __shared__ alignas(16) _Float16 patch2[3][kPatchChunks * 8];
+    __shared__ alignas(16) uint32_t imgs2[3][kImgWords];
+    __shared__ alignas(16) _Float16 bias[32 + 32 * MT];
+    const int t = (int)threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int n = lane & 31, h = lane >> 5;
+    const bool consumer = wid < 4;
+    const int G = (int)gridDim.x;
+    for (int i = t; i < 32 + 32 * MT; i += 512)
+        bias[i] = i < 32 ? (_Float16)a.b1[i] : (i - 32 < COUT ? (_Float16)a.b2[i - 32] : (_Float16)0.f);
+    int tile = (int)blockIdx.x;
+    if (tile >= a.ntiles) return;
+    if (consumer) {
+        h8 wa[kKS], wb[MT][2];
+#pragma unroll
+        for (int s = 0; s < kKS; ++s) wa[s] = *(const h8 *)(a.w1 + n * kK + 16 * s + 8 * h);
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) wb[m][s2] = *(const h8 *)(a.w2 + ((m * 2 + s2) * 32 + n) * 16 + 8 * h);
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();                               // (prologue: the producers' first halo)
+        __syncthreads();
+        for (int k = 0;; ++k) {
+            int b, y0, x0, ly0, lx0;
+            tile_coords(a, tile, b, y0, x0, ly0, lx0);
+            const _Float16 *halo = halo2[k & 1];
+            f16x acc[2] = {f16x{}, f16x{}};
+            auto bfrag = [&](int s, int r) -> h8 {
+                const int Gq = 2 * s + h;
+                if (Gq >= 45) return h8{};
+                const int tap = Gq / 5, q = Gq - 5 * tap, ky = tap / 3, kx = tap - 3 * ky;
+                return *(const h8 *)(halo + ((2 * wid + r + ky) * kHC + n + kx) * kCP + 8 * q);
+            };
+            // B fragments PVT_AHEAD k-steps ahead of their MFMAs (one consumer
+            // wave per SIMD: nothing else hides a fragment's LDS latency)
+            constexpr int AH = PVT_AHEAD;
+            h8 fb[AH + 1][2];
+#pragma unroll
+            for (int s = 0; s < AH; ++s) { fb[s][0] = bfrag(s, 0); fb[s][1] = bfrag(s, 1); }
+#pragma unroll
+            for (int s = 0; s < kKS; ++s) {
+                if (s + AH < kKS) {
+                    fb[(s + AH) % (AH + 1)][0] = bfrag(s + AH, 0);
+                    fb[(s + AH) % (AH + 1)][1] = bfrag(s + AH, 1);
+                }
+                const int c = s % (AH + 1);
+                acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa[s], fb[c][0], acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa[s], fb[c][1], acc[1], 0, 0, 0);
+            }
+            const __amdgpu_buffer_rsrc_t orr =
+                image_rsrc(a.out + (int64_t)b * a.H * a.W * COUT, (int64_t)a.H * a.W * COUT * 2);
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const int oy = y0 + 2 * wid + r, ox = x0 + n;
+                h8 act[2];
+#pragma unroll
+                for (int gq = 0; gq < 4; ++gq) {
+                    const h4 bq = *(const h4 *)(bias + 8 * gq + 4 * h);
+                    h4 y;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) y[j] = (_Float16)acc[r][4 * gq + j];
+                    y = y + bq;
+                    h4 ys;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) ys[j] = (_Float16)((float)y[j] * a.slope);
+                    y = __builtin_elementwise_max(y, ys);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) act[gq >> 1][4 * (gq & 1) + j] = y[j];
+                }
+                const int po = (oy < a.H && ox < a.W) ? (oy * a.W + ox) * (COUT * 2) : (int)0x80000000;
+#pragma unroll
+                for (int m = 0; m < MT; ++m) {
+                    f16x d = {};
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) d = __builtin_amdgcn_mfma_f32_32x32x16_f16(wb[m][s2], act[s2], d, 0, 0, 0);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int o0 = 32 * m + 8 * q + 4 * h;
+                        if (o0 + 3 < COUT) {
+                            h4 v;
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) v[j] = (_Float16)d[4 * q + j];
+                            v = v + *(const h4 *)(bias + 32 + o0);
+                            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), orr, po + 2 * o0, 0, 0);
+                        }
+                    }
+                }
+            }
+            __syncthreads();                           // this halo's reads are done; the next one is built
+            tile += G;
+            if (tile >= a.ntiles) break;
+        }
+        return;
+    }
+    // producers: wave pw = wid - 4 issues the DMA pieces a 4-wave block would
+    // (fetch's lane-linear layout); thread pt builds make_geo(pt)'s halo tasks
+    const int pw = wid - 4, pt = t - 256;
+    auto fetch2 = [&](int tl, _Float16 *patch, uint32_t *imgs) {
+        int b, y0, x0, ly0, lx0;
+        tile_coords(a, tl, b, y0, x0, ly0, lx0);
+        const __amdgpu_buffer_rsrc_t fr = image_rsrc(a.fm + (int64_t)b * a.Hin * a.Win * 32, (int64_t)a.Hin * a.Win * 64);
+        const int base = (ly0 * a.Win + lx0) * 64;
+#pragma unroll
+        for (int i = 0; i < kPatchIt; ++i) {
+            const int c0 = 256 * i + 64 * pw, c = c0 + lane;
+            if (c0 < kPatchChunks && c < kPatchChunks) {
+                const int pp = c >> 2, pr = pp / kPC;
+                const int off = base + pr * a.Win * 64 + (pp - pr * kPC) * 64 + 16 * (c & 3);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(fr, (__attribute__((address_space(3))) void *)(patch + 8 * c0),
+                                                         16, off, 0, 0, 0);
+            }
+        }
+        const __amdgpu_buffer_rsrc_t ir = image_rsrc(a.img + (int64_t)b * a.H * a.W * 3, (int64_t)a.H * a.W * 6);
+        const int ibase = ((y0 - 1) * a.W * 3 / 2 + x0 * 3 / 2 - 2) * 4;
+#pragma unroll
+        for (int i = 0; i < kImgIt; ++i) {
+            const int w0 = 256 * i + 64 * pw, w = w0 + lane;
+            if (w0 < kImgWords && w < kImgWords) {
+                const int r = w / kImgDw;
+                const int off = ibase + r * a.W * 6 + (w - r * kImgDw) * 4;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(ir, (__attribute__((address_space(3))) void *)(imgs + w0), 4,
+                                                         off, 0, 0, 0);
+            }
+        }
+    };
+    const Geo g = make_geo(pt);
+    auto build = [&](int tl, const _Float16 *patch, const uint32_t *imgs, _Float16 *halo) {
+        int b, y0, x0, ly0, lx0;
+        tile_coords(a, tl, b, y0, x0, ly0, lx0);
+        const int ox0 = x0 - 1 + (g.rc0 >> 2), ox1 = x0 - 1 + (g.rc1 >> 2);
+        const bool ok0 = ox0 >= 0 && ox0 < a.W, ok1 = ox1 >= 0 && ox1 < a.W;
+        const ColW w0 = col_weights(a, g.rc0, x0, lx0);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) halo_blend(a, patch, halo, w0, g.rc0, g.rhy0 + i, ok0, y0, ly0);
+        if (g.rx) halo_blend(a, patch, halo, col_weights(a, g.rc1, x0, lx0), g.rc1, g.rhy1, ok1, y0, ly0);
+        for (int p = pt; p < kHaloPx; p += 256) {
+            const int hy = p / kHC, hx = p - hy * kHC;
+            const int oy = y0 - 1 + hy, ox = x0 - 1 + hx;
+            h8 v = {};
+            if (oy >= 0 && oy < a.H && ox >= 0 && ox < a.W) {
+                const uint16_t *ip = (const uint16_t *)(imgs + hy * kImgDw) + 3 * hx + 1;
+                v[0] = __builtin_bit_cast(_Float16, ip[0]);
+                v[1] = __builtin_bit_cast(_Float16, ip[1]);
+                v[2] = __builtin_bit_cast(_Float16, ip[2]);
+            }
+            *(h8 *)(halo + p * kCP + 32) = v;
+        }
+    };
+    // tile i's patch and image rows in buffer i % 3: fetched in phase i - 2
+    // (after that phase's build), read in phase i - 1; a phase waits only for
+    // the previous phase's pieces (a counted vmcnt: wave 0 issues 6 pieces
+    // per tile, waves 1-3 four)
+    fetch2(tile, patch2[0], imgs2[0]);
+    if (tile + G < a.ntiles) fetch2(tile + G, patch2[1], imgs2[1]);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __syncthreads();                                   // every producer's pieces have landed
+    build(tile, patch2[0], imgs2[0], halo2[0]);
+    __syncthreads();
+    for (int k = 0;; ++k) {
+        const int t1 = tile + G, t2 = tile + 2 * G;
+        if (t1 < a.ntiles) build(t1, patch2[(k + 1) % 3], imgs2[(k + 1) % 3], halo2[(k + 1) & 1]);
+        if (t2 < a.ntiles) {
+            fetch2(t2, patch2[(k + 2) % 3], imgs2[(k + 2) % 3]);
+            if (pw == 0) __builtin_amdgcn_s_waitcnt(0x0F76);   // vmcnt(6): tile k + 2's in flight, k + 1's landed
+            else __builtin_amdgcn_s_waitcnt(0x0F74);           // vmcnt(4)
+        } else {
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+        }
+        __syncthreads();
+        tile = t1;
+        if (tile >= a.ntiles) break;
+    }
+}
+
 
 
 // ==========================================================================
@@ -434,7 +639,7 @@ struct ConvArgs {
 };
 
 // LDS image of a stage: row r's 16-byte segment s at granule 8 r + (s ^ (r & 7))
-__device__ __forceinline__ int conv_granule(int row, int seg) { return row * 8 + (seg ^ (row & 7)); }
+[[maybe_unused]] __device__ __forceinline__ int conv_granule(int row, int seg) { return row * 8 + (seg ^ (row & 7)); }
 
 // 16 bytes a lane from a buffer straight to LDS (wave-uniform LDS base + 16 x lane)
 __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_base, uint32_t voff, uint32_t soff) {
@@ -453,6 +658,9 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_ba
 #endif
 #ifndef PVC_FRAG_AHEAD
 #define PVC_FRAG_AHEAD 0         // 1: a step's fragments all read before its MFMAs (A/B, with PVC_NW=8)
+#endif
+#ifndef PVC_RING4
+#define PVC_RING4 0              // 1: k_conv3x3r, 32-channel half steps in a ring of four stages (A/B: bit-identical, measured ~25 % slower)
 #endif
 #ifndef PVC_PRIO
 #define PVC_PRIO 0               // 1: s_setprio(1) around each MFMA cluster (A/B)
@@ -803,6 +1011,160 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
 
 
 // --------------------------------------------------------------------------
+// k_conv3x3 with a four-stage ring of half steps (round 5): the same tiles,
+// tile order, split-K, epilogue and MFMA sequence (so the same sums, bit for
+// bit), but each 64-channel step's two 32-channel halves are staged
+// separately -- a stage is CT + 256 rows x 64 bytes (32 KiB at CT 256) -- in a
+// ring of four, and a half step's loads are issued three half steps before
+// it is consumed, right after the barrier that frees their stage.  The wait
+// before a half step is for its own loads only (a counted vmcnt: the two
+// newer half steps' stay in flight), so the loads' latency is covered by
+// three half steps of MFMAs instead of half a step (the 2-stage form issued
+// the next step's loads mid-step and waited for them at the next barrier).
+// LDS image: row r's 16-byte granule g at 4 r + (g ^ ((r >> 1) & 3))
+// (conflict-free for the 16x16x32 fragments' ds_read_b128).
+// --------------------------------------------------------------------------
+[[maybe_unused]] __device__ __forceinline__ int ring_granule(int row, int seg) { return row * 4 + (seg ^ ((row >> 1) & 3)); }
+
+template <int CT>
+__global__ __launch_bounds__(64 * kNW) void k_conv3x3r(ConvArgs a) {
+    constexpr int RB = 64;                                 // bytes per LDS row (32 channels)
+    constexpr int STAGE = (CT + kPT) * RB;                 // 32 KiB (CT 256), 24 KiB (CT 128)
+    constexpr int GPR = RB / 16;                           // 4 granules per row
+    constexpr int NI = (kPT * RB) / (1024 * kNW);          // pixel pieces per wave per stage: 1
+    constexpr int WPW = CT * RB / 1024;                    // weight pieces per stage: 16 (CT 256), 8 (CT 128)
+    constexpr int WC = kNW / 4;                            // cout groups of waves
+    constexpr int MI = CT / WC / 16;                       // 16-cout accumulator tiles per wave
+    static_assert(NI == 1 && WPW <= kNW, "one pixel piece per wave, at most one weight piece");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[4 * STAGE];
+    const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
+    const bool wload = wid < WPW;                          // this wave stages one weight piece per half step
+    int bid = (int)blockIdx.x, part = 0, tail = -1;
+    if (bid < a.nfull) {
+        const int nb = a.nfull, q = nb / 8, r = nb % 8, x = bid % 8;
+        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+    } else {
+        const int j = bid - a.nfull;
+        tail = j / a.nsplit;
+        part = j - tail * a.nsplit;
+        bid = a.nfull + tail;
+    }
+#if PVC_PT_MAJOR
+    const int ct = bid % a.nct, pt = bid / a.nct;
+#else
+    const int ct = bid / a.ntp, pt = bid % a.ntp;
+#endif
+    const int n0 = ct * CT;
+    const int64_t p0 = (int64_t)pt * kPT;
+    const __amdgpu_buffer_rsrc_t wr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.w, 0, (int)((int64_t)a.Cout * a.ksteps * 128), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)a.x, 0, (int)((int64_t)a.N * a.Hin * a.Win * a.Cin * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t x2r = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)a.x2, 0,
+        a.mode2 == PV_CONV_X2_1X1 ? (int)((int64_t)a.N * a.H2 * a.W2 * a.Cin2 * 2)
+                                  : (int)((int64_t)a.N * a.Hin * a.Win * a.Cin2 * 2),
+        0x00020000);
+    const int K2 = a.ksteps * 128;           // bytes per weight row
+    const int cbk = a.cblocks;
+    const int nmain2 = 2 * a.nmain;          // half steps of the 3x3 part
+    // this wave's weight piece (rows 16 wid .. +15) and pixel piece (rows 16 wid .. +15)
+    int woff = 0, pyb, pxb;
+    uint32_t pb1, pb2;
+    {
+        const int g = wid * 64 + lane, row = g / GPR, pseg = g % GPR;
+        const int seg = pseg ^ ((row >> 1) & 3);
+        woff = (n0 + row) * K2 + seg * 16;
+        const int64_t p = p0 + row;
+        const bool pin = p < a.M;
+        const int64_t pc = pin ? p : 0;
+        const int img = (int)(pc / ((int64_t)a.H * a.W)), rem = (int)(pc - (int64_t)img * a.H * a.W);
+        const int py = rem / a.W, px = rem - py * a.W;
+        pyb = pin ? py * a.stride : -(1 << 28);
+        pxb = px * a.stride;
+        const int pix = (img * a.Hin + py * a.stride) * a.Win + px * a.stride;
+        pb1 = (uint32_t)(pix * a.Cin * 2 + seg * 16);
+        if (a.mode2 == PV_CONV_X2_1X1)
+            pb2 = pin ? (uint32_t)(((img * a.H2 + py * a.s2) * a.W2 + px * a.s2) * a.Cin2 * 2 + seg * 16) : 0x80000000u;
+        else
+            pb2 = (uint32_t)(pix * a.Cin2 * 2 + seg * 16);
+    }
+    // half step h: 64-channel step s = h / 2 (channel block s / 9, tap s % 9, as
+    // k_conv3x3's PVC_CB_MAJOR order; the 1x1 part after it), channels
+    // 32 (h % 2) .. of it
+    auto issue = [&](int h, int buf) {
+        uint8_t *st = lds + buf * STAGE;
+        const int s = h >> 1, hf = h & 1;
+        if (wload) {
+            const int ks = s < a.nmain ? (s % 9) * cbk + s / 9 : s;
+            glds16(wr, st + wid * 1024, (uint32_t)woff, (uint32_t)(ks * 128 + hf * 64));
+        }
+        uint8_t *px = st + CT * RB + wid * 1024;
+        if (a.mode2 == PV_CONV_X2_1X1 && s >= a.nmain) {
+            glds16(x2r, px, pb2 + (uint32_t)((h - nmain2) * 64), 0);
+            return;
+        }
+        const int tap = s % 9, cb = s / 9;
+        const int dy = (tap / 3 - 1) * a.dil, dx = (tap % 3 - 1) * a.dil;
+        const bool second = a.mode2 == PV_CONV_X2_CAT && cb >= a.cb1;
+        const int C = second ? a.Cin2 : a.Cin, cbo = (second ? cb - a.cb1 : cb) * 128 + hf * 64;
+        const uint32_t delta = (uint32_t)((dy * a.Win + dx) * C * 2 + cbo);
+        const bool ok = (unsigned)(pyb + dy) < (unsigned)a.Hin && (unsigned)(pxb + dx) < (unsigned)a.Win;
+        const uint32_t off = ok ? (second ? pb2 : pb1) + delta : 0x80000000u;
+        glds16(second ? x2r : xr, px, off, 0);
+    };
+    const int wn = wid % WC, wm = wid / WC;
+    f4v acc[MI][4];
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f4v{0.f, 0.f, 0.f, 0.f};
+    auto compute = [&](const uint8_t *st) {
+        const int sg = lane >> 4;
+        h8v af[MI], bf[4];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) {
+            const int r = wn * (MI * 16) + mi * 16 + (lane & 15);
+            af[mi] = *(const h8v *)(st + ring_granule(r, sg) * 16);
+        }
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const int r = wm * 64 + ni * 16 + (lane & 15);
+            bf[ni] = *(const h8v *)(st + CT * RB + ring_granule(r, sg) * 16);
+        }
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+                acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mi], bf[ni], acc[mi][ni], 0, 0, 0);
+    };
+    const int ksteps = a.ksteps;
+    const int k0 = 2 * (tail < 0 ? 0 : part * ksteps / a.nsplit);
+    const int k1 = 2 * (tail < 0 ? ksteps : (part + 1) * ksteps / a.nsplit);
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+        if (k0 + u < k1) issue(k0 + u, u);
+    for (int h = k0; h < k1; ++h) {
+        // this wave's pieces of half step h have landed; those of the (up to)
+        // two half steps issued after it may still be in flight
+        const int ahead = min(2, k1 - 1 - h);
+        if (wload) {
+            if (ahead == 2) __builtin_amdgcn_s_waitcnt(0x0F74);        // vmcnt(4)
+            else if (ahead == 1) __builtin_amdgcn_s_waitcnt(0x0F72);   // vmcnt(2)
+            else __builtin_amdgcn_s_waitcnt(0x0F70);
+        } else {
+            if (ahead == 2) __builtin_amdgcn_s_waitcnt(0x0F72);        // vmcnt(2)
+            else if (ahead == 1) __builtin_amdgcn_s_waitcnt(0x0F71);   // vmcnt(1)
+            else __builtin_amdgcn_s_waitcnt(0x0F70);
+        }
+        __syncthreads();                       // ... and every wave's; half step h - 1's reads are done
+        if (h + 3 < k1) issue(h + 3, (h + 3 - k0) & 3);
+        compute(lds + ((h - k0) & 3) * STAGE);
+    }
+    conv_finish<CT, MI, WC>(a, acc, tail, part, n0, p0, wn, wm, lane, lds);
+}
+
+// --------------------------------------------------------------------------
 // The window form (stride 1, dilation <= kMaxDil): the same tiles, K order
 // (channel block, ky, kx) and epilogue as k_conv3x3, but a tile's pixel
 // operand for the three taps of one kernel row ky comes from ONE window of
@@ -1040,11 +1402,11 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3w(ConvArgs a) {
 // tile convolves.  Epilogue in registers: fp16 round of the f32 sums, + b,
 // LeakyReLU (y * slope in f32), 8-byte stores of 4 consecutive channels.
 // ==========================================================================
-constexpr int kDCo = 32, kDC1 = 64, kDC2 = 64;
-constexpr int kDOct = 9 * (kDC1 + kDC2) / 8;          // weight octets (16 bytes of 8 channels): 144
+[[maybe_unused]] constexpr int kDCo = 32, kDC1 = 64, kDC2 = 64;
+[[maybe_unused]] constexpr int kDOct = 9 * (kDC1 + kDC2) / 8;          // weight octets (16 bytes of 8 channels): 144
 constexpr int kDPatch = kPR * kPC * (kDC1 / 8);       // fm patch chunks: 1064
-constexpr int kDPatchIt = (kDPatch + 511) / 512;
-constexpr int kDTcol = kPR * kHC * (kDC1 / 8);        // column blends: 1904
+[[maybe_unused]] constexpr int kDPatchIt = (kDPatch + 511) / 512;
+[[maybe_unused]] constexpr int kDTcol = kPR * kHC * (kDC1 / 8);        // column blends: 1904
 constexpr int kDHalo = kHaloPx * 8;                   // halo chunks per part: 2720
 constexpr int kDSkipIt = (kDHalo + 511) / 512;
 
@@ -1059,6 +1421,9 @@ struct DecConvArgs {
 
 __device__ __forceinline__ int halo_granule(int hp, int q) { return hp * 8 + (q ^ (hp & 7)); }
 
+constexpr int kEC1 = 128, kECo = 64;                  // conv4s: fm channels, couts
+
+#if PVC_DEC_V1
 __global__ __launch_bounds__(512) void k_dec_conv2s(DecConvArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kDOct * kDCo * 16 + kDHalo * 16 + kDTcol * 16];
     uint8_t *wl = lds;                                  // 73,728 B
@@ -1238,7 +1603,6 @@ __global__ __launch_bounds__(512) void k_dec_conv2s(DecConvArgs a) {
 // part's 73.7 KB are loaded straight to LDS (buffer loads) while its halo is
 // built.
 // ==========================================================================
-constexpr int kEC1 = 128, kECo = 64;
 constexpr int kEWPart = 9 * 8 * kECo;                 // weight octets (16 B) per part: 4608
 constexpr int kEWIt = kEWPart * 16 / (1024 * 8);      // buffer-to-LDS loads per wave per part: 9
 
@@ -1404,6 +1768,342 @@ __global__ __launch_bounds__(512) void k_dec_conv4s(DecConvArgs a) {
                     for (int j = 0; j < 4; ++j) ys[j] = (_Float16)((float)y[j] * a.slope);
                     *(h4 *)(op + 32 * m + 8 * g + 4 * h) = __builtin_elementwise_max(y, ys);
                 }
+        }
+    }
+}
+
+#endif  // PVC_DEC_V1
+
+// ==========================================================================
+// The decoder steps conv4s / conv2s, warp-specialised (round 5): the same
+// operation as k_dec_conv4s / k_dec_conv2s above (up2(fm) + cat(., skip) + 3x3
+// conv + bias + LeakyReLU, fp16 channels-last), with the halo build and the
+// global loads no longer in sequence with the MFMAs.
+//
+// A tile (8 x 32 outputs of one image) is convolved in 32-channel parts: NUP
+// upsampled parts (fm channels 32p ..), then 2 skip parts.  Persistent blocks
+// of 16 waves, one per CU: waves 0-7 are consumers (wave = output row, 32
+// pixels x CO couts, 18 v_mfma_f32_32x32x16_f16 per part and 32 couts), waves
+// 8-15 producers.  One part per phase, one barrier per phase:
+//   consumers: LDS-DMA the NEXT part's weights (36 x CO x 16 B, from the
+//              host's [p64][9][8][CO][8] image) into the other weight buffer,
+//              the MFMAs of this part, the epilogue after the last part;
+//   producers: build the next part's halo (10 x 34 pixels x 32 channels,
+//              64 B a pixel, granule q ^ ((hp >> 2) & 3): conflict-free) in
+//              the other halo buffer -- an upsampled part blended from its
+//              7 x 19 fm patch (in one of two patch buffers, written two
+//              phases ahead from registers), a skip part copied from
+//              registers -- and issue the next tile's global loads.
+// The blend is pv_decoder_tail's / k_dec_conv2s's packed-fp16 separable
+// blend (two column blends, one row blend), bit for bit; the summation order
+// of the convolution is per 32-channel part (the former kernels: per 64).
+// LDS: 2 weight + 2 halo + 2 patch buffers = 97 KB (conv2s) / 134 KB (conv4s).
+// ==========================================================================
+constexpr int kXHalo = kHaloPx * 4;                   // halo chunks (16 B) per 32-channel part: 1360
+constexpr int kXHaloB = kXHalo * 16;                  // 21,760 B
+constexpr int kXPatch = kPR * kPC * 4;                // fm patch chunks per part: 532
+constexpr int kXPatchB = kXPatch * 16;                // 8,512 B
+constexpr int kXSkipIt = (kXHalo + 511) / 512;        // chunks per producer thread: 3
+constexpr int kXPatchIt = (kXPatch + 511) / 512;      // 2
+constexpr int kXBlendIt = (kXHalo + 511) / 512;       // 3
+
+__device__ __forceinline__ int halo32(int hp, int q) { return hp * 4 + (q ^ ((hp >> 2) & 3)); }
+
+#ifdef PVC_DEC_TRACE
+// trace builds only: per block, tile iteration < 4, phase < 6: s_memtime stamps
+// [0] consumer phase start, [1] consumer MFMAs issued/done, [2] consumer wait
+// done, [4] producer phase start, [5] producer loads issued, [6] producer
+// build done, [7] producer patch writes done
+__device__ unsigned long long *g_dec_trace;
+#define PVD_STAMP(it, j, k)                                                                                 \
+    if (g_dec_trace && (it) < 4 && lane == 0 && (wid == 0 || wid == 8))                                    \
+        g_dec_trace[(((int64_t)blockIdx.x * 4 + (it)) * 6 + (j)) * 8 + (k)] = __builtin_amdgcn_s_memtime()
+#else
+#define PVD_STAMP(it, j, k)
+#endif
+
+template <int CO, int NUP>
+__global__ __launch_bounds__(1024) void k_dec_conv(DecConvArgs a) {
+    constexpr int C1 = 32 * NUP;                       // fm channels
+    constexpr int P = NUP + 2;                         // parts per tile (even: buffer parity = part parity)
+    constexpr int WB = 36 * CO * 16;                   // one part's weights in LDS
+    constexpr int PIECES = WB / 1024;                  // LDS-DMA pieces per part (18 / 36)
+    constexpr int MT = CO / 32;                        // 32-cout accumulators per consumer
+    // the next tile's patch loads at phase 0 (conv2s) / 2 (conv4s: after this
+    // tile's parts 2, 3 are written), its skip loads at the last phase (after
+    // this tile's are consumed): one register set each
+    constexpr int LP = NUP == 2 ? 0 : 2, LS = P - 1, SS = 1;
+    static_assert(P % 2 == 0 && PIECES * 1024 == WB, "part parity and whole DMA pieces");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WB + 2 * kXHaloB + 2 * kXPatchB];
+    uint8_t *const wbuf = lds, *const hbuf = lds + 2 * WB, *const pbuf = lds + 2 * WB + 2 * kXHaloB;
+    const int t = (int)threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int n = lane & 31, h = lane >> 5;
+    const bool consumer = wid < 8;
+    const int pt = t - 512;                            // producer thread (0..511)
+    const int G = (int)gridDim.x;
+    auto coords = [&](int tile, int &b, int &y0, int &x0, int &ly0, int &lx0) {
+        const int tc = tile % a.tiles_c, rest = tile / a.tiles_c;
+        b = rest / a.tiles_r;
+        y0 = (rest % a.tiles_r) * kTR;
+        x0 = tc * kTC;
+        ly0 = (int)(a.rh * (float)max(y0 - 1, 0));
+        lx0 = (int)(a.rw * (float)max(x0 - 1, 0));
+    };
+    // ---- consumers: weights by LDS-DMA, MFMAs, epilogue ----
+    const __amdgpu_buffer_rsrc_t wr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.w, 0, (P / 2) * 9 * 8 * CO * 16, 0x00020000);
+    auto dma_weights = [&](int part) {                 // consumer waves: pieces wid, wid + 8, ...
+        uint8_t *dst = wbuf + (part & 1) * WB;
+        const int p64 = part >> 1, q0 = (part & 1) * 4;
+        for (int i = wid; i < PIECES; i += 8) {
+            const int byte = i * 1024 + lane * 16;
+            const int blk = byte / (CO * 16), within = byte - blk * (CO * 16);
+            const int tap = blk >> 2, q = blk & 3;
+            glds16(wr, dst + i * 1024, (uint32_t)(((p64 * 9 + tap) * 8 + q0 + q) * (CO * 16) + within), 0u);
+        }
+    };
+    h4 bq[MT][4];
+    if (consumer) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) bq[m][g] = *(const h4 *)(a.bias + 32 * m + 8 * g + 4 * h);
+    }
+    f16x acc[MT];
+    auto mfma_part = [&](int part) {
+        const uint8_t *W = wbuf + (part & 1) * WB, *Hb = hbuf + (part & 1) * kXHaloB;
+        auto frag = [&](int s, h8 &bf, h8 (&af)[MT]) {
+            const int o = 2 * s + h, tap = o >> 2, q = o & 3;
+            const int ky = tap / 3, kx = tap - 3 * ky;
+            bf = *(const h8 *)(Hb + halo32((wid + ky) * kHC + n + kx, q) * 16);
+#pragma unroll
+            for (int m = 0; m < MT; ++m) af[m] = *(const h8 *)(W + ((tap * 4 + q) * CO + 32 * m + n) * 16);
+        };
+        constexpr int AH = PVC_DEC_AHEAD;
+        h8 fb[AH + 1], fa[AH + 1][MT];
+#pragma unroll
+        for (int s = 0; s < AH; ++s) frag(s, fb[s], fa[s]);
+#pragma unroll
+        for (int s = 0; s < 18; ++s) {
+            if (s + AH < 18) frag(s + AH, fb[(s + AH) % (AH + 1)], fa[(s + AH) % (AH + 1)]);
+            const int c = s % (AH + 1);
+#pragma unroll
+            for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[c][m], fb[c], acc[m], 0, 0, 0);
+        }
+    };
+    auto epilogue = [&](int tile) {
+        int b, y0, x0, ly0, lx0;
+        coords(tile, b, y0, x0, ly0, lx0);
+        const int oy = y0 + wid, ox = x0 + n;
+        if (oy < a.H && ox < a.W) {
+            _Float16 *op = a.out + (((int64_t)b * a.H + oy) * a.W + ox) * CO;
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    h4 y;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) y[j] = (_Float16)acc[m][4 * g + j];
+                    y = y + bq[m][g];
+                    h4 ys;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) ys[j] = (_Float16)((float)y[j] * a.slope);
+                    *(h4 *)(op + 32 * m + 8 * g + 4 * h) = __builtin_elementwise_max(y, ys);
+                }
+        }
+    };
+    // ---- producers: loads into registers, patch writes, halo builds ----
+    h8 preg[2][kXPatchIt], sreg[SS][2][kXSkipIt];
+    // a tile's fm patches of up parts [u0, u1) (part u into slot u & 1) / skip
+    // halo (both parts) into registers; a tile past the last reads nothing
+    // (out-of-range offsets)
+    auto load_patch = [&](int tile, int u0, int u1) {
+        int b, y0, x0, ly0, lx0;
+        coords(min(tile, a.ntiles - 1), b, y0, x0, ly0, lx0);
+        const __amdgpu_buffer_rsrc_t fr = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(a.fm + (int64_t)b * a.Hin * a.Win * C1), 0, a.Hin * a.Win * C1 * 2, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < kXPatchIt; ++i) {
+            const int c = min(pt + 512 * i, kXPatch - 1), pp = c >> 2, q = c & 3;
+            const int pr = pp / kPC, pc = pp - pr * kPC;
+            const uint32_t off = tile < a.ntiles ? (uint32_t)(((ly0 + pr) * a.Win + lx0 + pc) * (C1 * 2) + q * 16)
+                                                 : 0x80000000u;   // rows past fm read 0
+            for (int u = u0; u < u1; ++u)
+                preg[u & 1][i] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(fr, off, u * 64, 0));
+        }
+    };
+    auto load_skip = [&](int tile, h8 (&sr)[2][kXSkipIt]) {
+        int b, y0, x0, ly0, lx0;
+        coords(min(tile, a.ntiles - 1), b, y0, x0, ly0, lx0);
+        const __amdgpu_buffer_rsrc_t sr_ = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(a.skip + (int64_t)b * a.H * a.W * 64), 0, a.H * a.W * 64 * 2, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < kXSkipIt; ++i) {
+            const int c = min(pt + 512 * i, kXHalo - 1), hp = c >> 2, q = c & 3;
+            const int hy = hp / kHC, hx = hp - hy * kHC;
+            const int oy = y0 - 1 + hy, ox = x0 - 1 + hx;
+            const bool ok = tile < a.ntiles && oy >= 0 && oy < a.H && ox >= 0 && ox < a.W;
+            const uint32_t off = ok ? (uint32_t)((oy * a.W + ox) * 128 + q * 16) : 0x80000000u;
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                sr[u][i] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(sr_, off, u * 64, 0));
+        }
+    };
+    auto write_patch = [&](int up) {                   // up part `up`'s patch -> patch buffer up & 1
+        uint8_t *pb = pbuf + (up & 1) * kXPatchB;
+#pragma unroll
+        for (int i = 0; i < kXPatchIt; ++i)
+            if (pt + 512 * i < kXPatch) *(h8 *)(pb + (pt + 512 * i) * 16) = preg[up & 1][i];
+    };
+    auto build_skip = [&](int sp, int part, const h8 (&sr)[2][kXSkipIt]) {
+        uint8_t *hb = hbuf + (part & 1) * kXHaloB;
+#pragma unroll
+        for (int i = 0; i < kXSkipIt; ++i) {
+            const int c = pt + 512 * i;
+            if (c < kXHalo) *(h8 *)(hb + halo32(c >> 2, c & 3) * 16) = sr[sp][i];
+        }
+    };
+    // the blend tasks of this producer thread: halo chunks pt + 512 i, i < 3
+    // (the last only for pt < 336) -- pixel (thy[i], thx[i]), octet pt & 3;
+    // tile independent
+    int thy[kXBlendIt], thx[kXBlendIt];
+#pragma unroll
+    for (int i = 0; i < kXBlendIt; ++i) {
+        const int hp = (pt + 512 * i) >> 2;
+        thy[i] = hp / kHC;
+        thx[i] = hp - thy[i] * kHC;
+    }
+    auto build_up = [&](int tile, int part) {          // blend of patch buffer part & 1 -> halo buffer part & 1
+        int b, y0, x0, ly0, lx0;
+        coords(tile, b, y0, x0, ly0, lx0);
+        const uint8_t *pb = pbuf + (part & 1) * kXPatchB;
+        uint8_t *hb = hbuf + (part & 1) * kXHaloB;
+        const int q = pt & 3;
+        // tasks [i0, i1): their four patch reads each first (their LDS
+        // latencies overlap), then the blends; a halo pixel outside the image
+        // reads a clamped one and stores zero
+        auto tasks = [&](auto I0, auto I1) {
+            constexpr int i0 = decltype(I0)::value, i1 = decltype(I1)::value;
+            h8 A[i1 - i0], B[i1 - i0], C[i1 - i0], D[i1 - i0];
+            float wl[i1 - i0], hl[i1 - i0];
+            bool in[i1 - i0];
+#pragma unroll
+            for (int i = i0; i < i1; ++i) {
+                const int k = i - i0;
+                const int oy = y0 - 1 + thy[i], ox = x0 - 1 + thx[i];
+                in[k] = oy >= 0 && oy < a.H && ox >= 0 && ox < a.W;
+                const int oyc = min(max(oy, 0), a.H - 1), oxc = min(max(ox, 0), a.W - 1);
+                const float w1r = a.rw * (float)oxc, h1r = a.rh * (float)oyc;
+                const int w1 = (int)w1r, h1 = (int)h1r;
+                const int dw = w1 < a.Win - 1 ? 4 : 0, dh = h1 < a.Hin - 1 ? kPC * 4 : 0;
+                wl[k] = w1r - (float)w1;
+                hl[k] = h1r - (float)h1;
+                const uint8_t *pp = pb + (((h1 - ly0) * kPC + (w1 - lx0)) * 4 + q) * 16;
+                A[k] = *(const h8 *)pp;
+                B[k] = *(const h8 *)(pp + dw * 16);
+                C[k] = *(const h8 *)(pp + dh * 16);
+                D[k] = *(const h8 *)(pp + (dh + dw) * 16);
+            }
+#pragma unroll
+            for (int i = i0; i < i1; ++i) {
+                const int k = i - i0;
+                const int c = pt + 512 * i;
+                if (c >= kXHalo) break;
+                const h8 ww = (h8)(_Float16)wl[k], w0 = (h8)(_Float16)(1.f - wl[k]);
+                const h8 c0 = __builtin_elementwise_fma(B[k], ww, A[k] * w0);
+                const h8 c1 = __builtin_elementwise_fma(D[k], ww, C[k] * w0);
+                h8 v = __builtin_elementwise_fma(c1, (h8)(_Float16)hl[k], c0 * (h8)(_Float16)(1.f - hl[k]));
+                if (!in[k]) v = h8{};
+                *(h8 *)(hb + halo32(c >> 2, q) * 16) = v;
+            }
+        };
+        static_assert(kXBlendIt == 3, "tasks 0-1, then 2");
+        tasks(std::integral_constant<int, 0>{}, std::integral_constant<int, 2>{});
+        tasks(std::integral_constant<int, 2>{}, std::integral_constant<int, 3>{});
+    };
+
+    int tile = (int)blockIdx.x;
+    if (tile >= a.ntiles) return;
+    // The two roles run separate loops (so that their registers -- the
+    // accumulators and fragments, the prefetched inputs -- share the file)
+    // with the same barriers: two in the prologue, one per phase.
+    if (consumer) {
+        dma_weights(0);                                // part 0's weights
+        __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0)
+        __syncthreads();
+        __syncthreads();
+        for (int it = 0;; ++it) {
+            (void)it;
+            const bool more = tile + G < a.ntiles;
+#pragma unroll
+            for (int m = 0; m < MT; ++m) acc[m] = f16x{};
+#pragma unroll 1     // (unrolled, the phases' fragment and DMA registers overlap: spills at MT = 2)
+            for (int j = 0; j < P; ++j) {
+                PVD_STAMP(it, j, 0);
+                if (j + 1 < P || more) dma_weights((j + 1) % P);
+                mfma_part(j);
+                if (j == P - 1) epilogue(tile);
+                PVD_STAMP(it, j, 1);
+                __builtin_amdgcn_s_waitcnt(0x0F70);    // this wave's weight pieces (and stores) have landed
+                PVD_STAMP(it, j, 2);
+                __syncthreads();
+            }
+            tile += G;
+            if (!more) break;
+        }
+        return;
+    }
+    // producers.  Prologue: tile 0's inputs, its patches 0 and 1 written,
+    // part 0 built
+    load_patch(tile, 0, 2);
+    load_skip(tile, sreg[0]);
+    write_patch(0);
+    write_patch(1);
+    if (NUP == 4) load_patch(tile, 2, 3);              // (part 3: at this tile's phase 0)
+    __syncthreads();
+    build_up(tile, 0);
+    __syncthreads();
+    // one tile: P phases (part j consumed, part j + 1 built), one barrier each
+    [[maybe_unused]] int it = 0;                       // (trace builds: the tile iteration)
+    auto tile_body = [&](auto SET) {
+        constexpr int S = decltype(SET)::value;        // this tile's skip register set
+        constexpr int SN = (S + 1) % SS;               // the next tile's
+        const int nxt = tile + G;
+        const bool more = nxt < a.ntiles;
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            PVD_STAMP(it, j, 4);
+            const int m = j + 1;                       // the part this phase builds
+            if (m < NUP) build_up(tile, m);
+            else if (m < P) build_skip(m - NUP, m, sreg[S]);
+            else if (more) build_up(nxt, 0);
+            PVD_STAMP(it, j, 5);
+            // patches two phases ahead of their builds
+            if (j + 2 < NUP) write_patch(j + 2);
+            else if (j >= P - 2) write_patch(j - (P - 2));
+            PVD_STAMP(it, j, 6);
+            // global loads last: a wave's instructions issue in order, and a
+            // load waiting for room in the memory pipeline would hold the build
+            // behind it.  Patch registers, two slots: conv2s the next tile's
+            // parts 0-1 at phase 0; conv4s its parts 0-1 at phase 2, its part 2
+            // at phase 5 (once this tile's parts are written), this tile's part
+            // 3 at phase 0 (used at phase 1)
+            if (j == LP) load_patch(nxt, 0, 2);        // (past the last tile: no access)
+            if (NUP == 4 && j == P - 1) load_patch(nxt, 2, 3);
+            if (NUP == 4 && j == 0) load_patch(tile, 3, 4);
+            if (j == LS) load_skip(nxt, sreg[SN]);
+            PVD_STAMP(it, j, 7);
+            __syncthreads();
+        }
+        tile = nxt;
+        ++it;
+        return more;
+    };
+    if constexpr (SS == 2) {
+        while (tile_body(std::integral_constant<int, 0>{}) && tile_body(std::integral_constant<int, 1>{})) {
+        }
+    } else {
+        while (tile_body(std::integral_constant<int, 0>{})) {
         }
     }
 }
@@ -1579,10 +2279,16 @@ extern "C" int pv_decoder_tail_f16(const void *fm, const void *img, const void *
 #ifdef PVT_TRACE
     a.trace = g_tail_trace;
 #endif
-    const int64_t grid = std::min<int64_t>(nt, (int64_t)PVT_WPE * cu_count_dec());   // persistent: PVT_WPE blocks per CU
     hipStream_t s = (hipStream_t)stream;
+#if PVT_V1
+    const int64_t grid = std::min<int64_t>(nt, (int64_t)PVT_WPE * cu_count_dec());   // persistent: PVT_WPE blocks per CU
     if (cout == 20) k_decoder_tail<20><<<(unsigned)grid, 256, 0, s>>>(a);
     else k_decoder_tail<44><<<(unsigned)grid, 256, 0, s>>>(a);
+#else
+    const int64_t grid2 = std::min<int64_t>(nt, cu_count_dec());   // persistent: one block per CU
+    if (cout == 20) k_decoder_tail2<20><<<(unsigned)grid2, 512, 0, s>>>(a);
+    else k_decoder_tail2<44><<<(unsigned)grid2, 512, 0, s>>>(a);
+#endif
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? PV_OK : (int)e;
 }
@@ -1606,7 +2312,10 @@ ConvSplit conv_split(int64_t pixels, int32_t cout, int32_t ksteps) {
     int S = rem > 0 ? (int)std::min<int64_t>(4, cus / rem) : 1;
     while (S > 1 && ksteps / S < 4) --S;          // parts of at least 4 K-steps
     if (S < 2) return ConvSplit{(int)ntiles, 1, 0, 0};
-    const int64_t tb = (rem * 4 + 255) / 256 * 256;
+    // the counters' region has one size for every call (4 KiB: up to 1,024
+    // split tiles), so that a scratch shared by calls of different shapes
+    // never has one call's partials over another's counters
+    const int64_t tb = std::max<int64_t>(4096, (rem * 4 + 255) / 256 * 256);
     // one tile's partials: its CT x 256 f32 sums (each of the 64 kNW threads
     // holds CT / kNW 16-byte groups), per part
     const int64_t per = (int64_t)S * (wide ? kCT : 128) * kPT * 4;
@@ -1693,8 +2402,13 @@ extern "C" int pv_conv3x3_ex_f16(const void *x, int32_t hin, int32_t win, int32_
     } else
 #endif
     {
+#if PVC_RING4
+        if (wide) k_conv3x3r<kCT><<<grid, 64 * kNW, 0, (hipStream_t)stream>>>(a);
+        else k_conv3x3r<128><<<grid, 64 * kNW, 0, (hipStream_t)stream>>>(a);
+#else
         if (wide) k_conv3x3<kCT><<<grid, 64 * kNW, 0, (hipStream_t)stream>>>(a);
         else k_conv3x3<128><<<grid, 64 * kNW, 0, (hipStream_t)stream>>>(a);
+#endif
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? PV_OK : (int)e;
@@ -1729,10 +2443,20 @@ extern "C" int pv_decoder_conv2s_f16(const void *fm, const void *skip, const voi
     a.rw = (float)(win - 1) / (float)(a.W - 1);
     a.slope = slope;
     const int64_t grid = std::min<int64_t>(nt, cu_count_dec());   // persistent: one block per CU
+#if PVC_DEC_V1
     k_dec_conv2s<<<(unsigned)grid, 512, 0, (hipStream_t)stream>>>(a);
+#else
+    k_dec_conv<32, 2><<<(unsigned)grid, 1024, 0, (hipStream_t)stream>>>(a);
+#endif
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? PV_OK : (int)e;
 }
+
+#ifdef PVC_DEC_TRACE
+extern "C" int pv_debug_set_dec_trace(void *p) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_dec_trace), &p, sizeof(p));
+}
+#endif
 
 extern "C" int pv_decoder_conv4s_f16(const void *fm, const void *skip, const void *w, const void *bias, void *out,
                                      int32_t n, int32_t hin, int32_t win, float slope, pv_stream_t stream) {
@@ -1755,7 +2479,11 @@ extern "C" int pv_decoder_conv4s_f16(const void *fm, const void *skip, const voi
     a.rw = (float)(win - 1) / (float)(a.W - 1);
     a.slope = slope;
     const int64_t grid = std::min<int64_t>(nt, cu_count_dec());   // persistent: one block per CU
+#if PVC_DEC_V1
     k_dec_conv4s<<<(unsigned)grid, 512, 0, (hipStream_t)stream>>>(a);
+#else
+    k_dec_conv<64, 4><<<(unsigned)grid, 1024, 0, (hipStream_t)stream>>>(a);
+#endif
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? PV_OK : (int)e;
 }

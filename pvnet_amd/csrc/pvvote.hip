@@ -1782,6 +1782,15 @@ __device__ inline bool lu2_inv(float a00, float a01, float a10, float a11, float
 // ticket add per block; the last block's wave 0 reads them with sc1 loads
 // (MI355X_MICROARCH.md "Valid forms", row 1).
 // ==========================================================================
+#ifdef PVV_TRACE
+__device__ uint64_t *g_refine_trace;   // trace builds only: per-block phase stamps of k_refine_solve
+#define PVR_STAMP(k)                                                                                      \
+    if (g_refine_trace && threadIdx.x == 0)                                                               \
+        g_refine_trace[(((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 8 + (k)] = \
+            __builtin_amdgcn_s_memrealtime()
+#else
+#define PVR_STAMP(k)
+#endif
 __global__ __launch_bounds__(kRT) void k_refine_solve(const int32_t *counts, const float2 *hyp, const float4 *pex,
                                                       const int32_t *tn, int64_t P, int vn, int nh,
                                                       float thr, int32_t *win_out, float *ratio_out, double *refpart,
@@ -1789,6 +1798,7 @@ __global__ __launch_bounds__(kRT) void k_refine_solve(const int32_t *counts, con
                                                       float *out,
                                                       pv_v3_diag diag) {
     const int j = blockIdx.x, v = blockIdx.y, b = blockIdx.z;
+    PVR_STAMP(0);
     const int n = min(max(tn[b], 0), (int)P);   // clamped like tn_at: loads stay inside the P records
     __shared__ uint64_t skey[kRW];
     __shared__ double sacc[kRW][5];
@@ -1826,6 +1836,7 @@ __global__ __launch_bounds__(kRT) void k_refine_solve(const int32_t *counts, con
     }
     if (lane_id() == 0) skey[threadIdx.x / 64] = key;
     __syncthreads();
+    PVR_STAMP(1);
     key = skey[0];
     for (int q = 1; q < kRW; ++q) key = skey[q] > key ? skey[q] : key;
     const int win = (int)(0xffffffffu - (uint32_t)key);
@@ -1850,12 +1861,14 @@ __global__ __launch_bounds__(kRT) void k_refine_solve(const int32_t *counts, con
     for (int u = 0; u < U; ++u)
         if (t0 + u * tstep < n) accum(e[u]);
     for (int t = t0 + U * tstep; t < n; t += tstep) accum(eb[t]);   // images larger than U * tstep
+    PVR_STAMP(2);
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
         double s = wave_sum_d(acc[k]);
         if (lane_id() == 0) sacc[threadIdx.x / 64][k] = s;
     }
     __syncthreads();
+    PVR_STAMP(3);
     // Hand-off: every block publishes its partials and takes a ticket of its
     // image; the image's last block sums each keypoint's kRefineNJ partials
     // (in a fixed order: deterministic) and solves them all.  (A ticket per
@@ -1881,6 +1894,7 @@ __global__ __launch_bounds__(kRT) void k_refine_solve(const int32_t *counts, con
         if (k == 0) slast = (t == vn * kRefineNJ - 1);
     }
     __syncthreads();
+    PVR_STAMP(4);
     if (!slast) return;
     // ---- last block of image b: each keypoint's kRefineNJ partials (consecutive
     // records = an aligned lane group) summed by a fixed shuffle tree, and the keypoints'
@@ -1919,6 +1933,7 @@ __global__ __launch_bounds__(kRT) void k_refine_solve(const int32_t *counts, con
         }
     }
     __syncthreads();
+    PVR_STAMP(5);
     if (threadIdx.x >= 64) return;
     // ---- solve for every keypoint (lane = keypoint) ----
     const int vv = threadIdx.x;
@@ -1967,6 +1982,7 @@ __global__ __launch_bounds__(kRT) void k_refine_solve(const int32_t *counts, con
             diag.iters[b] = it;
         }
     }
+    PVR_STAMP(6);
 }
 
 // ==========================================================================
@@ -3484,6 +3500,8 @@ int pv_debug_lookback_self(int32_t on) {
 #ifdef PVV_TRACE
 // trace builds only: per-wave timestamps of the next pipeline vote launches
 void pv_debug_set_vote_trace(uint64_t *buf) { g_vote_trace = buf; }
+// trace builds only: per-block phase stamps of the next k_refine_solve launches
+int pv_debug_set_refine_trace(uint64_t *buf) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_refine_trace), &buf, sizeof(buf)); }
 #endif
 // test hook (not in pvvote.h): which fused vote/count kernel the pipeline runs
 // (0 matrix-core k_vote_mfma, 1 VALU k_vote_count); returns the previous

@@ -405,6 +405,7 @@ def conv3x3(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, dil: int, act:
 _CONV_WS: dict = {}         # eager calls: (device, stream) -> [buffers]
 _CAPTURE_WS: dict = {}      # inside a capture: (device, stream, capture id) -> the graph's own buffer
 _CONV_WS_LOCK = threading.Lock()     # per-GPU threads (DataParallel-style callers) share the tables
+_CAPTURE_WS_BYTES = (64 << 20) + 4096
 
 
 def clear_conv_workspaces() -> None:
@@ -447,8 +448,11 @@ def _conv_workspace(x: torch.Tensor, pixels: int, cout: int, ksteps: int):
                 del _CAPTURE_WS[k]      # an earlier capture's: its graph's pool keeps the memory
             buf = _CAPTURE_WS.get(key)
             if buf is None or buf.numel() < need:
-                buf = torch.empty(need, dtype=torch.uint8, device=x.device)
-                nc = int(L.pv_conv3x3_workspace_counter_bytes(pixels, cout, ksteps))
+                # sized for any split of the capture's later convolutions too (at
+                # most one split tile per CU, 4 parts of 256 x 256 f32 partials:
+                # 64 MiB), so the capture takes one counter fill, not one per size
+                buf = torch.empty(max(need, _CAPTURE_WS_BYTES), dtype=torch.uint8, device=x.device)
+                nc = int(L.pv_conv3x3_workspace_counter_bytes(pixels, cout, ksteps))   # 4 KiB for every shape
                 buf[:nc].zero_()        # captured: runs at every replay, before this call's kernel
                 _CAPTURE_WS[key] = buf
             return buf.data_ptr(), buf.numel()

@@ -1004,3 +1004,45 @@ def test_conv_split_scratch_capture_without_warmup(device):
     B.check(e1, y64, e, "eager after capture")
     B.check(got_g, y64, e, "captured (replayed)")
     clear_conv_workspaces()
+
+
+@pytest.mark.gpu
+def test_conv_split_scratch_shared_by_two_shapes(device):
+    """One stream's split-K scratch serves convolutions of different shapes in
+    turn (network._conv_workspace keeps one per stream): shape A (100 split
+    tiles on 256 CUs), shape B (30 split tiles), A again.  B's partials must
+    not land on A's arrival counters (the counters' region has one size for
+    every shape, pvvote.h), so the second A equals the first bit for bit, and
+    both are within the fp16 bound of the f64 convolution."""
+    from pvnet_amd import _lib
+    from pvnet_amd.network import clear_conv_workspaces, conv3x3, conv3x3_weight
+    g = torch.Generator().manual_seed(606)
+    cl = torch.channels_last
+    cin, cout = 128, 128
+    conv = torch.nn.Conv2d(cin, cout, 3, 1, 1, bias=True)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5))
+        conv.bias.copy_(torch.randn(cout, generator=g) * 0.5)
+    conv = conv.to(device).half()
+    wt = conv3x3_weight(conv)
+    xa = torch.randn(1, cin, 178, 512, generator=g).to(device, torch.float16).contiguous(memory_format=cl)
+    xb = torch.randn(1, cin, 143, 512, generator=g).to(device, torch.float16).contiguous(memory_format=cl)
+    L = _lib.load()
+    assert L.pv_conv3x3_workspace_bytes(178 * 512, cout, 18) > 0 and L.pv_conv3x3_workspace_bytes(143 * 512, cout, 18) > 0
+    clear_conv_workspaces()
+    s = torch.cuda.Stream(device=device)
+    with torch.no_grad(), torch.cuda.stream(s):
+        a1 = conv3x3(xb, wt, conv.bias, 1, "relu")           # B first: the scratch grows to A's size below
+        a1 = conv3x3(xa, wt, conv.bias, 1, "relu")
+        conv3x3(xb, wt, conv.bias, 1, "relu")
+        a2 = conv3x3(xa, wt, conv.bias, 1, "relu")
+    s.synchronize()
+    assert torch.equal(a1, a2)
+    with torch.no_grad():
+        c64 = B.conv64(xa, conv.weight, padding=1)
+        e = B.round_step(c64, B.acc_bound(xa, conv.weight, 9 * cin, padding=1))
+        y64 = c64 + conv.bias.double().view(1, -1, 1, 1)
+        e = B.round_step(y64, e)
+        y64 = torch.relu(y64)
+    B.check(a2, y64, e, "split scratch shared by two shapes")
+    clear_conv_workspaces()
