@@ -52,22 +52,27 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kCompactChunk = 256;           // pixels per compaction block (one per thread)
 constexpr int kVoteChunk = 256;              // pixels per LDS-staged sub-chunk of the vote waves
-// refine blocks per (image, keypoint); measured on the 8-in-flight stream
-// (tools/ab_libs.sh, two rounds): 32 -> 42.4-42.8k images/s, 16 -> 43.0-43.1k,
-// 8 -> 43.4-43.7k, 4 -> 37.3-37.5k, 2 -> 33.0-33.2k (fewer blocks hold fewer
-// CU slots while they wait on memory; below 8 a block's serial work shows)
+// refine blocks per (image, keypoint); measured with the gathering hand-off
+// (tools/ab_libs.sh, two rounds, stream images/s and sequential latency):
+// 16 -> 53.8-54.0k / 47.7-48.6 us, 32 -> 53.2-53.3k / 47.5-48.2 us; with the
+// round-4 ticket hand-off 8 -> 52.7k / 50.9-51.8 us, 16 -> 53.0k / 50.8-51.2,
+// 32 -> 52.5-52.7k / 51.1-51.6 (the round-4 kernel itself: 52.5-52.7k / 52.1)
 #ifndef PVV_REFINE_NJ
-#define PVV_REFINE_NJ 8
+#define PVV_REFINE_NJ 16
 #endif
 constexpr int kRefineNJ = PVV_REFINE_NJ;
 #ifndef PVV_REFINE_T
 #define PVV_REFINE_T 256
 #endif
-// refine block threads (tools/lat_ab.sh, same threads per keypoint, two rounds:
-// 8 x 256 43.3-43.8k images/s / 51.9 us sequential latency, 16 x 128 43.0k /
-// 53.6-53.9 us, 32 x 64 41.6k / 59.5 us)
+// refine block threads (round 5, 16 blocks per keypoint: 256 -> 53.6-53.9k
+// images/s, 512 -> 52.7-53.6k, 1024 -> 44.5k / 50.5 us; round 4, same threads
+// per keypoint: 8 x 256 43.3-43.8k / 51.9 us, 16 x 128 43.0k / 53.6-53.9 us,
+// 32 x 64 41.6k / 59.5 us)
 constexpr int kRT = PVV_REFINE_T;
-constexpr int kRW = kRT / 64;                // ... in waves
+// a refine block's published partial: 5 least-squares sums (fp64) + its winner
+// (ratio, index), each value as one 16-B pair of tagged 8-B granules
+constexpr int kRefineGran = 6;
+constexpr int kRefineLdsHyp = 1024;          // hypotheses per keypoint kept in LDS (more: k_refine_solve<true>)
 // domain of the fast test's error bound
 constexpr float kHypMax = 1.0e17f;           // |hx|,|hy| above -> exact-only hypothesis
 constexpr float kLattice = 2.5e-6f;          // |h - round(h)| below (both axes) -> exact-only
@@ -94,6 +99,30 @@ __device__ __forceinline__ bool exact_vote(float nx, float ny, float cx, float c
     if (below_1e6(norm1) || below_1e6(norm2)) return false;
     float angle_dist = (dx * nx + dy * ny) / (norm1 * norm2);
     return angle_dist > thr;
+}
+
+// exact_vote's decision for K6's one hypothesis per keypoint, settled by a
+// squared comparison where that is provably the same (*und: not settled, the
+// exact sequence must decide): on the domain below
+// (squared norms in [1e-11, 1e18]: KU's 1e-6 guards pass, nothing over- or
+// underflows) the exact sequence's angle is dot / (|n| |d|) within 4 roundings
+// (2.4e-7 relative) and dot^2 / (thr^2 |n|^2 |d|^2) is within 5 roundings of
+// its square, so outside a 2e-6 band around equality both decide alike;
+// inside the band, outside the domain, or for thr outside [1e-3, 1] (`fast`
+// false), the exact sequence decides.  `thr2` = thr * thr.
+__device__ __forceinline__ void refine_vote_pre(float nx, float ny, float cx, float cy, float hx, float hy,
+                                                float thr2, bool fast, bool *inl, bool *und) {
+    const float dx = hx - cx, dy = hy - cy;
+    const float nn1 = nx * nx + ny * ny;
+    const float nn2 = dx * dx + dy * dy;
+    const float dot = dx * nx + dy * ny;   // the exact sequence's numerator, bit for bit
+    const bool dom = fast && nn1 >= 1e-11f && nn1 <= 1e18f && nn2 >= 1e-11f && nn2 <= 1e18f;
+    const float l = dot * dot, r = thr2 * nn1 * nn2;
+    const bool pos = dot > 0.f;            // else angle <= 0 < thr (or NaN): outlier
+    const bool in = pos && l > r * (1.f + 2e-6f);
+    const bool out = !pos || l < r * (1.f - 2e-6f);
+    *inl = dom && in;
+    *und = !dom || !(in || out);
 }
 
 // KU:28-48: intersection of the lines through two pixels. false = degenerate.
@@ -196,10 +225,10 @@ __device__ __forceinline__ bool is_fg(const MaskView &m, int b, int r, int c) {
 // --------------------------------------------------------------------------
 struct Workspace {
     int32_t *counts;    // [b][vn][nh]   zeroed by k_fg_count
-    int32_t *ticket;    // [b][1 + vn]   zeroed by k_fg_count: per image, per (image, keypoint)
+    uint4 *refslot;     // [b][vn][kRefineNJ][kRefineGran] zeroed by k_fg_count: k_refine_solve's tagged partials
     int32_t *dsagg;     // [b][nblk]     zeroed by k_fg_count: downsampled count + 1 per block (look-back)
     int32_t *confc;     // [b][vn][2]    zeroed by k_fg_count: v5 confidence count, ticket
-    int64_t zero_words; // counts + ticket + dsagg + confc (contiguous)
+    int64_t zero_words; // counts + refslot + dsagg + confc (contiguous)
     int32_t *tn;        // [b] compacted pixels (0 = image skipped)
     int32_t *fgtot;     // [b] foreground before downsampling
     int32_t *blkcnt;    // [b][nblk]
@@ -207,10 +236,6 @@ struct Workspace {
     float4 *pex;        // [b][vn][P]   exact pixel data (cx, cy, nx, ny): reference operands
     float2 *hyp;        // [b][nh][vn]  (reference layout)
     float2 *hypv;       // [b][vn][nh]  keypoint-major copy (pre-generated hypotheses)
-    int32_t *win;       // [b][vn]
-    float *ratio;       // [b][vn]
-    double *refpart;    // [b][vn][kRefineNJ][5]
-    double *ksum;       // [b][vn][5]  least-squares sums per keypoint
     size_t total;
 };
 
@@ -221,10 +246,12 @@ Workspace carve(void *base, int b, int H, int W, int vn, int nh) {
     char *p = (char *)base;
     int64_t off = 0;
     auto take = [&](int64_t bytes) { char *q = p ? p + off : nullptr; off = align_up(off + bytes, 256); return q; };
-    w.zero_words = (int64_t)b * vn * nh + (int64_t)b * (1 + vn) + b * nblk + 2 * (int64_t)b * vn;
+    const int64_t ncnt = align_up((int64_t)b * vn * nh, 4);            // refslot 16-B aligned
+    const int64_t nslot = (int64_t)b * vn * kRefineNJ * kRefineGran;
+    w.zero_words = ncnt + 4 * nslot + b * nblk + 2 * (int64_t)b * vn;
     w.counts = (int32_t *)take(4 * w.zero_words);
-    w.ticket = w.counts ? w.counts + (int64_t)b * vn * nh : nullptr;
-    w.dsagg = w.counts ? w.ticket + (int64_t)b * (1 + vn) : nullptr;
+    w.refslot = w.counts ? (uint4 *)(w.counts + ncnt) : nullptr;
+    w.dsagg = w.counts ? (int32_t *)(w.refslot + nslot) : nullptr;
     w.confc = w.counts ? w.dsagg + b * nblk : nullptr;
     w.tn = (int32_t *)take(4 * b);
     w.fgtot = (int32_t *)take(4 * b);
@@ -233,10 +260,6 @@ Workspace carve(void *base, int b, int H, int W, int vn, int nh) {
     w.pex = (float4 *)take(16 * b * vn * P);
     w.hyp = (float2 *)take(8 * (int64_t)b * nh * vn);
     w.hypv = (float2 *)take(8 * (int64_t)b * nh * vn);
-    w.win = (int32_t *)take(4 * b * vn);
-    w.ratio = (float *)take(4 * b * vn);
-    w.refpart = (double *)take(8 * 5 * (int64_t)b * vn * kRefineNJ);
-    w.ksum = (double *)take(8 * 5 * (int64_t)b * vn);
     w.total = (size_t)off;
     return w;
 }
@@ -256,6 +279,37 @@ __device__ __forceinline__ int wave_sum_i(int x) {
 }
 __device__ __forceinline__ double wave_sum_d(double x) {
     for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+// sum over each 16-lane row of the wave (every lane of a row gets its row's
+// sum) by DPP moves: xor 1, xor 2, half-row mirror, row mirror -- VALU
+// operations, not the LDS-routed ds_bpermute of __shfl_xor
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, x);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, true);
+    return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t u) {
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, true);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+__device__ __forceinline__ uint64_t row_max_u64(uint64_t x) {
+    uint64_t o;
+    o = dpp_u64<0xB1>(x); x = o > x ? o : x;
+    o = dpp_u64<0x4E>(x); x = o > x ? o : x;
+    o = dpp_u64<0x141>(x); x = o > x ? o : x;
+    o = dpp_u64<0x140>(x); x = o > x ? o : x;
+    return x;
+}
+__device__ __forceinline__ double row_sum_d(double x) {
+    x += dpp_d<0xB1>(x);    // quad_perm [1,0,3,2]
+    x += dpp_d<0x4E>(x);    // quad_perm [2,3,0,1]
+    x += dpp_d<0x141>(x);   // row_half_mirror: quad q <-> 1-q within each half row
+    x += dpp_d<0x140>(x);   // row_mirror: half rows swapped
     return x;
 }
 // sum over the block of (x, y); `sh` holds >= 8 ints
@@ -1775,12 +1829,15 @@ __device__ inline bool lu2_inv(float a00, float a01, float a10, float a11, float
 
 // ==========================================================================
 // K6: winner per (image, keypoint) (RV:567-575) + least-squares partial sums
-// over the winner's inliers (RV:584-599, fp64), then -- in the last block of
-// each image to finish -- b_inv with its batch-wide identity fallback
-// (RV:503-518) and pts = b_inv(ATA) @ ATb (RV:600).
-// Hand-off: partials stored write-through (sc1) and drained, one agent-scope
-// ticket add per block; the last block's wave 0 reads them with sc1 loads
-// (MI355X_MICROARCH.md "Valid forms", row 1).
+// over the winner's inliers (RV:584-599, fp64), kRefineNJ blocks per
+// keypoint; the last block of each image gathers its image's partials, sums
+// them per keypoint in a fixed order, solves (pts = b_inv(ATA) @ ATb, RV:600)
+// with b_inv's batch-wide identity fallback (RV:503-518).
+// Hand-off (cdna_hip_programming.md Guideline 16, R2: the data is the flag):
+// every value travels as 8-B granules {32-bit half, tag}, a pair per 16-B
+// sc1 store; the gathering block re-reads them with 16-B sc1 loads until
+// every tag is set.  The granules are zeroed by k_fg_count every call; no
+// ticket, no drain before a signal, one memory trip from publish to use.
 // ==========================================================================
 #ifdef PVV_TRACE
 __device__ uint64_t *g_refine_trace;   // trace builds only: per-block phase stamps of k_refine_solve
@@ -1791,19 +1848,39 @@ __device__ uint64_t *g_refine_trace;   // trace builds only: per-block phase sta
 #else
 #define PVR_STAMP(k)
 #endif
-__global__ __launch_bounds__(kRT) void k_refine_solve(const int32_t *counts, const float2 *hyp, const float4 *pex,
-                                                      const int32_t *tn, int64_t P, int vn, int nh,
-                                                      float thr, int32_t *win_out, float *ratio_out, double *refpart,
-                                                      double *ksum, int32_t *ticket, float confidence, int max_iter,
-                                                      float *out,
-                                                      pv_v3_diag diag) {
+constexpr uint32_t kRefineTag = 1u;           // granule tag (slots zeroed every call)
+constexpr uint32_t kRefineSpinMax = 1u << 21;  // gather polls before giving up (~seconds): outputs NaN
+// BIG: nh > 1024 hypotheses (the winner's is fetched, not kept in LDS; the
+// counts beyond the first 1024 read in a loop) -- its own instantiation, so
+// the common one has no loop whose loads would make the compiler drain every
+// load in flight before the argmax
+template <bool BIG>
+__global__ __launch_bounds__(kRT) void k_refine_solve(const int32_t *counts, const float2 *hyp, int64_t hsb, int hsv,
+                                                      int hsh, const float4 *pex, const int32_t *tn, int64_t P, int vn,
+                                                      int nh, float thr, uint4 *slot, float confidence, int max_iter,
+                                                      float *out, pv_v3_diag diag) {
     const int j = blockIdx.x, v = blockIdx.y, b = blockIdx.z;
     PVR_STAMP(0);
+    __shared__ uint64_t skey[kRT / 16];
+    __shared__ double sacc[kRT / 16][5];   // row sums (16-lane rows)
+    constexpr int HC = kRefineLdsHyp / kRT;         // counts / hypotheses per thread, in registers
+    static_assert(kRefineLdsHyp % kRT == 0, "PVV_REFINE_T divides the LDS hypothesis capacity");
+    __shared__ float2 shyp[kRefineLdsHyp];
+    // Loads are issued in the order they are needed and return in that order:
+    // the pixel count, the keypoint's vote counts and hypotheses (the argmax
+    // needs only those), then this block's pixels (the winner's votes).
     const int n = min(max(tn[b], 0), (int)P);   // clamped like tn_at: loads stay inside the P records
-    __shared__ uint64_t skey[kRW];
-    __shared__ double sacc[kRW][5];
-    __shared__ int slast;
-    // this block's pixels, loaded before the argmax so both latencies overlap
+    const int32_t *cnt = counts + ((int64_t)b * vn + v) * nh;
+    const float2 *hb = hyp + b * hsb + (int64_t)v * hsv;
+    constexpr bool lds_hyp = !BIG;
+    int32_t c[HC];
+    float2 hh[HC];
+    // (every load unconditional, its index clamped into range, so that no
+    // branch makes the compiler wait for all of them before the first use)
+#pragma unroll
+    for (int q = 0; q < HC; ++q) c[q] = cnt[min((int)threadIdx.x + q * kRT, nh - 1)];
+#pragma unroll
+    for (int q = 0; q < HC; ++q) hh[q] = hb[(int64_t)min((int)threadIdx.x + q * kRT, nh - 1) * hsh];
     constexpr int U = 32768 / (kRefineNJ * kRT);    // 32768 pixels per keypoint preloaded
     static_assert(U >= 1, "PVV_REFINE_NJ * PVV_REFINE_T must not exceed 32768 (preload depth)");
     static_assert(kRT % 64 == 0 && kRT <= 1024, "PVV_REFINE_T: whole waves, at most 1024 threads");
@@ -1813,146 +1890,178 @@ __global__ __launch_bounds__(kRT) void k_refine_solve(const int32_t *counts, con
     const int t0 = j * kRT + threadIdx.x, tstep = kRefineNJ * kRT;
     float4 e[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int t = t0 + u * tstep;
-        e[u] = t < P ? eb[t] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    // the keypoint's hypotheses too (the winner's is then read from LDS, not
-    // fetched after the argmax: one memory round trip fewer)
-    constexpr int kRefineLdsHyp = 1024;
-    __shared__ float2 shyp[kRefineLdsHyp];
-    if (nh <= kRefineLdsHyp)
-        for (int h = threadIdx.x; h < nh; h += kRT) shyp[h] = hyp[((int64_t)b * nh + h) * vn + v];
+    for (int u = 0; u < U; ++u) e[u] = eb[min(t0 + u * tstep, (int)P - 1)];
     // argmax over h, first index on ties: key = count << 32 | ~h
     uint64_t key = 0;
-    const int32_t *cnt = counts + ((int64_t)b * vn + v) * nh;
-    for (int h = threadIdx.x; h < nh; h += kRT) {
-        uint64_t k2 = ((uint64_t)(uint32_t)cnt[h] << 32) | (uint32_t)(0xffffffffu - (uint32_t)h);
+    auto take = [&](int32_t cv, int h) {
+        const uint64_t k2 = ((uint64_t)(uint32_t)cv << 32) | (uint32_t)(0xffffffffu - (uint32_t)h);
         key = k2 > key ? k2 : key;
+    };
+#pragma unroll
+    for (int q = 0; q < HC; ++q) {
+        const int h = (int)threadIdx.x + q * kRT;
+        take(h < nh ? c[q] : 0, h < nh ? h : -1);   // out of range: key 0 (the initial value)
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        uint64_t other = __shfl_xor(key, o);
-        key = other > key ? other : key;
-    }
-    if (lane_id() == 0) skey[threadIdx.x / 64] = key;
+    if constexpr (BIG)
+        for (int h = (int)threadIdx.x + kRefineLdsHyp; h < nh; h += kRT) take(cnt[h], h);
+    if constexpr (lds_hyp)
+#pragma unroll
+        for (int q = 0; q < HC; ++q)
+            if ((int)threadIdx.x + q * kRT < nh) shyp[threadIdx.x + q * kRT] = hh[q];
+    key = row_max_u64(key);                      // DPP within 16-lane rows, rows through LDS
+    if ((lane_id() & 15) == 0) skey[threadIdx.x / 16] = key;
     __syncthreads();
     PVR_STAMP(1);
     key = skey[0];
-    for (int q = 1; q < kRW; ++q) key = skey[q] > key ? skey[q] : key;
+#pragma unroll
+    for (int q = 1; q < kRT / 16; ++q) key = skey[q] > key ? skey[q] : key;
     const int win = (int)(0xffffffffu - (uint32_t)key);
     const int wcnt = (int)(key >> 32);
     // RV:570-575: ratio = count / tn; best starts at 0 and is replaced only on a strict increase
     const float ratio = n > 0 ? (float)wcnt / (float)n : 0.f;
     float2 best = make_float2(0.f, 0.f);
-    if (n > 0 && 0.f < ratio) best = nh <= kRefineLdsHyp ? shyp[win] : hyp[((int64_t)b * nh + win) * vn + v];
+    if (n > 0 && 0.f < ratio) best = lds_hyp ? shyp[win] : hb[(int64_t)win * hsh];
+#ifdef PVV_TRACE
+    if (g_refine_trace) {   // trace builds: when the block's pixels have arrived
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PVR_STAMP(7);
+    }
+#endif
     double acc[5] = {0, 0, 0, 0, 0};
-    auto accum = [&](const float4 &q) {   // (cx, cy, nx, ny)
-        if (exact_vote(q.z, q.w, q.x, q.y, best.x, best.y, thr)) {
-            float n0 = q.w, n1 = -q.z;                  // RV:585-587 normal = (d_y, -d_x)
-            float bb = n0 * q.x + n1 * q.y;             // RV:597 (2-term fp32 sum)
-            acc[0] += (double)n0 * n0;
-            acc[1] += (double)n0 * n1;
-            acc[2] += (double)n1 * n1;
-            acc[3] += (double)n0 * bb;
-            acc[4] += (double)n1 * bb;
+    const bool fast = thr >= 1e-3f && thr <= 1.f;
+    const float thr2 = thr * thr;
+    // branch-free: the squared pre-test decides by selects; the exact sequence
+    // runs only when some lane of the wave is undecided; an outlier adds zeros
+    auto accum = [&](const float4 &q, bool valid) {   // (cx, cy, nx, ny)
+        bool inl, und;
+        refine_vote_pre(q.z, q.w, q.x, q.y, best.x, best.y, thr2, fast, &inl, &und);
+        und = und && valid;
+        if (__ballot(und)) {
+            if (und) inl = exact_vote(q.z, q.w, q.x, q.y, best.x, best.y, thr);
         }
+        inl = inl && valid;
+        const float n0 = inl ? q.w : 0.f, n1 = inl ? -q.z : 0.f;   // RV:585-587 normal = (d_y, -d_x)
+        const float bb = inl ? q.w * q.x + -q.z * q.y : 0.f;       // RV:597 (2-term fp32 sum)
+        // f32 x f32 is exact in f64, so each fma equals the product-then-add
+        const double d0 = n0, d1 = n1, db = bb;
+        acc[0] = __fma_rn(d0, d0, acc[0]);
+        acc[1] = __fma_rn(d0, d1, acc[1]);
+        acc[2] = __fma_rn(d1, d1, acc[2]);
+        acc[3] = __fma_rn(d0, db, acc[3]);
+        acc[4] = __fma_rn(d1, db, acc[4]);
     };
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-        if (t0 + u * tstep < n) accum(e[u]);
-    for (int t = t0 + U * tstep; t < n; t += tstep) accum(eb[t]);   // images larger than U * tstep
+    for (int u = 0; u < U; ++u) accum(e[u], t0 + u * tstep < n);
+    for (int t = t0 + U * tstep; t < n; t += tstep) accum(eb[t], true);   // images larger than U * tstep
     PVR_STAMP(2);
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-        double s = wave_sum_d(acc[k]);
-        if (lane_id() == 0) sacc[threadIdx.x / 64][k] = s;
+        const double sr = row_sum_d(acc[k]);
+        if ((lane_id() & 15) == 0) sacc[threadIdx.x / 16][k] = sr;
     }
     __syncthreads();
     PVR_STAMP(3);
-    // Hand-off: every block publishes its partials and takes a ticket of its
-    // image; the image's last block sums each keypoint's kRefineNJ partials
-    // (in a fixed order: deterministic) and solves them all.  (A ticket per
-    // keypoint and then per image took two more memory round trips.)
-    int32_t *tk_img = ticket + (int64_t)b * (1 + vn);
-    if (threadIdx.x < 64) {   // wave 0: publish this block's partials, then take a ticket
+    // ---- publish: this block's partial, the data as its own flag ----
+    const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(slot + (int64_t)b * vn * kRefineNJ * kRefineGran), (short)0, 0x7fffffff, 0x00020000);
+    static_assert(kRefineNJ <= 32, "gather: one pending bit per partial");
+    if (threadIdx.x < kRefineGran) {
         const int k = threadIdx.x;
-        double *rp = refpart + (((int64_t)b * vn + v) * kRefineNJ + j) * 5;
+        uint64_t bits;
         if (k < 5) {
             double sk = sacc[0][k];
 #pragma unroll
-            for (int q = 1; q < kRW; ++q) sk += sacc[q][k];
-            st_agent(&rp[k], sk);
+            for (int q = 1; q < kRT / 16; ++q) sk += sacc[q][k];
+            bits = __builtin_bit_cast(uint64_t, sk);
+        } else {
+            bits = ((uint64_t)(uint32_t)(n > 0 ? win : 0) << 32) | __float_as_uint(ratio);
         }
-        if (j == 0 && k == 0) {
-            st_agent(&win_out[b * vn + v], n > 0 ? win : 0);
-            st_agent(&ratio_out[b * vn + v], ratio);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        int t = 0;
-        if (k == 0) t = __hip_atomic_fetch_add(tk_img, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        t = __shfl(t, 0);
-        if (k == 0) slast = (t == vn * kRefineNJ - 1);
+        typedef int v4i __attribute__((ext_vector_type(4)));
+        const v4i g = {(int)(uint32_t)bits, (int)kRefineTag, (int)(uint32_t)(bits >> 32), (int)kRefineTag};
+        __builtin_amdgcn_raw_buffer_store_b128(g, sr, ((v * kRefineNJ + j) * kRefineGran + k) * 16, 0, 16);   // sc1
     }
-    __syncthreads();
+    if (j == 0 && threadIdx.x == 0) {
+        if (diag.win_ratio) diag.win_ratio[b * vn + v] = n > 0 ? ratio : 0.f;
+        if (diag.win_idx) diag.win_idx[b * vn + v] = n > 0 ? win : 0;
+    }
     PVR_STAMP(4);
-    if (!slast) return;
-    // ---- last block of image b: each keypoint's kRefineNJ partials (consecutive
-    // records = an aligned lane group) summed by a fixed shuffle tree, and the keypoints'
-    // winners and ratios, all loads in flight together ----
-    static_assert(kRefineNJ >= 2 && kRefineNJ <= 64 && (kRefineNJ & (kRefineNJ - 1)) == 0,
-                  "a keypoint's partials fill an aligned lane group");
+    // the image's highest block gathers: dispatched last (in practice: only
+    // speed depends on it), it mostly finds every partial already there
+    if (j != kRefineNJ - 1 || v != vn - 1) return;
+    // ---- gather.  Thread p polls value k of keypoint vv in a quarter of the
+    // kRefineNJ partials (its loads in flight together); sums in partial
+    // order, quarters then in order: deterministic ----
+    constexpr int kGQ = kRefineNJ >= 4 ? 4 : kRefineNJ, kGJ = kRefineNJ / kGQ;
     __shared__ double sks[64][5];
+    __shared__ double sq[64 * kRefineGran * kGQ];
     __shared__ float srat[64];
-    __shared__ int swin[64];
-    {
-        const double *rp = refpart + (int64_t)b * vn * kRefineNJ * 5;
-        const int nrec = vn * kRefineNJ;
-        constexpr int R = 2;                  // rounds in flight together (vn <= 16: all of them)
-        for (int r0 = 0; r0 < nrec; r0 += R * kRT) {
-            double s5[R][5];
+    __shared__ int sflag;   // bit 0: some matrix singular, bit 1: gather gave up
+    if (threadIdx.x == 0) sflag = 0;
+    __syncthreads();
+    bool gave_up = false;
+    for (int p = threadIdx.x; p < vn * kRefineGran * kGQ; p += kRT) {
+        const int vk = p / kGQ, jq = p - vk * kGQ;
+        const int vv = vk / kRefineGran, k = vk - vv * kRefineGran;
+        const int base = (vv * kRefineNJ + jq * kGJ) * kRefineGran + k;
+        uint64_t val[kGJ];
+        uint32_t pend = (1u << kGJ) - 1;
+        for (uint32_t spins = 0; pend; ++spins) {
+            typedef int v4i __attribute__((ext_vector_type(4)));
+            v4i g[kGJ];
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int i = r0 + r * kRT + (int)threadIdx.x;
+            for (int jj = 0; jj < kGJ; ++jj)
+                if (pend >> jj & 1) g[jj] = __builtin_amdgcn_raw_buffer_load_b128(sr, (base + jj * kRefineGran) * 16, 0, 16);
 #pragma unroll
-                for (int q = 0; q < 5; ++q) s5[r][q] = i < nrec ? ld_agent(&rp[i * 5 + q]) : 0.0;
-            }
-            if (r0 == 0 && threadIdx.x < (unsigned)vn) {
-                srat[threadIdx.x] = ld_agent(&ratio_out[b * vn + threadIdx.x]);
-                swin[threadIdx.x] = ld_agent(&win_out[b * vn + threadIdx.x]);
-            }
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int i = r0 + r * kRT + (int)threadIdx.x;
-#pragma unroll
-                for (int q = 0; q < 5; ++q)
-                    for (int o = kRefineNJ / 2; o > 0; o >>= 1) s5[r][q] += __shfl_xor(s5[r][q], o);
-                if ((lane_id() & (kRefineNJ - 1)) == 0 && i < nrec)
-#pragma unroll
-                    for (int q = 0; q < 5; ++q) sks[i / kRefineNJ][q] = s5[r][q];
-            }
+            for (int jj = 0; jj < kGJ; ++jj)
+                if ((pend >> jj & 1) && (uint32_t)g[jj].y == kRefineTag && (uint32_t)g[jj].w == kRefineTag) {
+                    val[jj] = ((uint64_t)(uint32_t)g[jj].z << 32) | (uint32_t)g[jj].x;
+                    pend &= ~(1u << jj);
+                }
+            if (pend && spins >= kRefineSpinMax) { gave_up = true; break; }
+            if (pend) __builtin_amdgcn_s_sleep(2);
         }
+        if (gave_up) break;
+        if (k < 5) {
+            double sum = __builtin_bit_cast(double, val[0]);
+#pragma unroll
+            for (int jj = 1; jj < kGJ; ++jj) sum += __builtin_bit_cast(double, val[jj]);
+            sq[p] = sum;
+        } else if (jq == 0) {
+            srat[vv] = __uint_as_float((uint32_t)val[0]);   // every block of a keypoint finds the same winner
+        }
+    }
+    if (gave_up) sflag = 2;   // benign race: every writer stores 2
+    __syncthreads();
+    for (int q = threadIdx.x; q < vn * 5; q += kRT) {
+        const int vv = q / 5, k = q - vv * 5;
+        const double *sp = &sq[(vv * kRefineGran + k) * kGQ];
+        double sum = sp[0];
+#pragma unroll
+        for (int jq = 1; jq < kGQ; ++jq) sum += sp[jq];
+        sks[vv][k] = sum;
     }
     __syncthreads();
     PVR_STAMP(5);
-    if (threadIdx.x >= 64) return;
-    // ---- solve for every keypoint (lane = keypoint) ----
+    // ---- solve, one thread per keypoint (vn <= 64: wave 0) ----
     const int vv = threadIdx.x;
     const bool act = vv < vn;
     float A00 = 0, A01 = 0, A11 = 0, B0 = 0, B1 = 0, rat = 3.0e38f;
-    int wi = 0;
+    float inv[4] = {1.f, 0.f, 0.f, 1.f};
     if (act) {
         A00 = (float)sks[vv][0]; A01 = (float)sks[vv][1]; A11 = (float)sks[vv][2];
         B0 = (float)sks[vv][3]; B1 = (float)sks[vv][4];
         rat = srat[vv];
-        wi = swin[vv];
+        if (!lu2_inv(A00, A01, A01, A11, inv)) atomicOr(&sflag, 1);
     }
-    float inv[4] = {1.f, 0.f, 0.f, 1.f};
-    bool ok = act ? lu2_inv(A00, A01, A01, A11, inv) : true;
-    if (!__all(ok)) { inv[0] = 1.f; inv[1] = 0.f; inv[2] = 0.f; inv[3] = 1.f; }   // RV:514-517
+    __syncthreads();
+    if (threadIdx.x >= 64) return;
+    const int flag = sflag;
+    if (flag & 1) { inv[0] = 1.f; inv[1] = 0.f; inv[2] = 0.f; inv[3] = 1.f; }   // RV:514-517
     if (act) {
         float x = inv[0] * B0 + inv[1] * B1;
         float y = inv[2] * B0 + inv[3] * B1;
         if (n == 0) { x = 0.f; y = 0.f; }
+        if (flag & 2) { x = __int_as_float(0x7fc00000); y = x; }   // gather gave up: loud
         out[((int64_t)b * vn + vv) * 2] = x;
         out[((int64_t)b * vn + vv) * 2 + 1] = y;
         if (diag.ata) {
@@ -1960,15 +2069,13 @@ __global__ __launch_bounds__(kRT) void k_refine_solve(const int32_t *counts, con
             q[0] = A00; q[1] = A01; q[2] = A01; q[3] = A11;
         }
         if (diag.atb) { diag.atb[((int64_t)b * vn + vv) * 2] = B0; diag.atb[((int64_t)b * vn + vv) * 2 + 1] = B1; }
-        if (diag.win_ratio) diag.win_ratio[b * vn + vv] = n > 0 ? rat : 0.f;
-        if (diag.win_idx) diag.win_idx[b * vn + vv] = wi;
     }
-    // min ratio over keypoints -> iterations the reference's `while True` would run
-    float r = rat;
-    for (int o = 32; o > 0; o >>= 1) r = fminf(r, __shfl_xor(r, o));
-    if (vv == 0) {
-        if (diag.tn) diag.tn[b] = n;
-        if (diag.iters) {
+    if (diag.tn && vv == 0) diag.tn[b] = n;
+    if (diag.iters) {
+        // min ratio over keypoints -> iterations the reference's `while True` would run
+        float r = rat;
+        for (int o = 32; o > 0; o >>= 1) r = fminf(r, __shfl_xor(r, o));
+        if (vv == 0) {
             int it = 0;
             if (n > 0) {
                 long long hyp_num = 0;
@@ -3126,6 +3233,11 @@ static_assert(PVV_VM_BPC >= 1 && PVV_VM_BPC <= 4, "k_vote_mfma: 1..4 blocks per 
 int g_vote_kernel = 0;    // 0: k_vote_mfma (hn a multiple of 512), 1: k_vote_count
 int g_bytes_dbg = 0;
 bool vote_old() { return g_vote_kernel == 1; }
+// does front_half pre-generate the hypotheses (k_hyp_gen, keypoint-major in w.hypv)?
+bool hyp_pregen_used(int vn, int nh) {
+    (void)vn;
+    return PVV_HYPGEN && ((nh + kGroup - 1) / kGroup) % 4 == 0 && !vote_old();
+}
 
 template <bool PREPPED>
 void launch_vote(const VoteArgs &va, int64_t pixel_steps, hipStream_t s) {
@@ -3272,7 +3384,7 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
     // prologue, overlapped with its first pixel loads) and stores them in
     // the reference layout; by default (hyp_pregen) one k_hyp_gen launch makes
     // them first and the vote kernel (k_vote_mfma) reads them keypoint-major
-    if (PVV_HYPGEN && va.hgn % 4 == 0 && !vote_old()) {
+    if (hyp_pregen_used(vn, nh)) {
         va.hypv_out = w.hypv;
         const int64_t nt = (int64_t)b * nh * vn;
         k_hyp_gen<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(va);
@@ -3546,9 +3658,12 @@ int pv_ransac_voting_v3(const pv_image_desc *img, const pv_vote_params *prm, flo
     if ((r = front_half(img, prm, nh, false, w, dg, s))) return r;
     const int b = img->b, vn = img->vn;
     const int64_t P = (int64_t)img->H * img->W;
-    k_refine_solve<<<dim3(kRefineNJ, vn, b), kRT, 0, s>>>(w.counts, w.hyp, w.pex, w.tn, P, vn, nh,
-                                                          prm->inlier_thresh, w.win, w.ratio, w.refpart, w.ksum,
-                                                          w.ticket,
+    // hypotheses keypoint-major when the pipeline pre-generated them (coalesced), else the reference layout
+    const bool hv = hyp_pregen_used(vn, nh);
+    auto *kref = nh > kRefineLdsHyp ? k_refine_solve<true> : k_refine_solve<false>;
+    kref<<<dim3(kRefineNJ, vn, b), kRT, 0, s>>>(w.counts, hv ? w.hypv : w.hyp, (int64_t)nh * vn,
+                                                          hv ? nh : 1, hv ? 1 : vn, w.pex, w.tn, P, vn, nh,
+                                                          prm->inlier_thresh, w.refslot,
                                                           prm->confidence, prm->max_iter, out, dg);
     if ((r = last())) return r;
     if (dg.counts) {

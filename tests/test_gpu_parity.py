@@ -303,6 +303,57 @@ def test_v3_synth_full_size(hn, device, rvg):
     assert int(diag["iters"][0]) == int(g["iters"])
 
 
+def _angles_f32(direct, coords, hyp):
+    """KU:107-125's per-pixel sequence in float32 (numpy rounds each op like
+    the kernel): the angle of each pixel's direction to the hypothesis, NaN
+    where a norm guard rejects it.  direct/coords [tn,2], hyp [2]."""
+    F = np.float32
+    dx = F(hyp[0]) - coords[:, 0]
+    dy = F(hyp[1]) - coords[:, 1]
+    nx, ny = direct[:, 0], direct[:, 1]
+    n1 = np.sqrt(nx * nx + ny * ny)
+    n2 = np.sqrt(dx * dx + dy * dy)
+    with np.errstate(all="ignore"):
+        a = (dx * nx + dy * ny) / (n1 * n2)
+    a[(n1 <= F(1e-6)) | (n2 <= F(1e-6))] = np.nan
+    return a
+
+
+@pytest.mark.parametrize("case", ["cat_v3_512", "synth_v3_512"])
+@pytest.mark.parametrize("thr_mode", ["default", "boundary"])
+def test_v3_refine_sums_match_oracle(case, thr_mode, device, rvg):
+    """K6's least-squares sums (diag ata / atb) equal the oracle's (RV:584-599,
+    correctly rounded) over the winner's inlier set -- one pixel in or out
+    would move them by ~1/tn.  "boundary": the threshold is set to the exact
+    float32 angle of some pixels to the first keypoint's winner, so those
+    pixels sit exactly on the cone's edge (angle == thr: outliers) and the
+    kernel's squared pre-test must hand them to the exact sequence."""
+    g = G.load(case)
+    mask, vertex = (G.cat_inputs(g) if case.startswith("cat") else G.synth_inputs(g))[:2]
+    coords, direct = O.compact(O.fg_mask_v3(mask[0]), vertex[0])
+    idxs = g["idxs"]
+    thr = 0.99
+    if thr_mode == "boundary":
+        d0 = {}
+        rvg.ransac_voting_layer_v3(cu(mask, device), cu(vertex, device), 512, _idxs=idxs, _diag=d0)
+        w0 = int(d0["win_idx"].cpu().numpy()[0, 0])
+        hyp0 = d0["hyp"].cpu().numpy()[0, w0, 0]
+        a = _angles_f32(direct[:, 0], coords, hyp0)
+        cand = np.sort(a[np.isfinite(a) & (a > 0.9) & (a < 1.0)])
+        thr = float(cand[len(cand) // 2])
+        assert np.count_nonzero(a == np.float32(thr)) >= 1
+    diag = {}
+    rvg.ransac_voting_layer_v3(cu(mask, device), cu(vertex, device), 512, inlier_thresh=thr, _idxs=idxs,
+                               _diag=diag)
+    diag = {k: v.cpu().numpy() for k, v in diag.items()}
+    vn = vertex.shape[3]
+    win_pts = diag["hyp"][0][diag["win_idx"][0], np.arange(vn)]
+    win_pts[diag["win_ratio"][0] <= 0] = 0
+    _, ata, atb = O.refine(direct, coords, win_pts.astype(np.float32), np.float32(thr))
+    np.testing.assert_allclose(diag["ata"][0].reshape(vn, 2, 2), ata, rtol=1e-6, atol=1e-7 * np.abs(ata).max())
+    np.testing.assert_allclose(diag["atb"][0].reshape(vn, 2), atb, rtol=1e-6, atol=1e-7 * np.abs(atb).max())
+
+
 def test_v3_from_network_fused(device, rvg):
     """seg_pred/vertex_pred straight from the network layout (argmax fused)."""
     g = G.load("synth_v3_512")

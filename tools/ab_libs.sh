@@ -4,7 +4,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 for rep in 1 2; do
   for v in "$@"; do
-    PVVOTE_LIB=variants/$v.so timeout -k 10 200 python bench.py --steps 50 --warmup 10 --skip-cpu --skip-e2e --skip-u1 --skip-config3 > gpurun_out/ab_$v.$rep.log 2>&1 || exit $?
+    PVVOTE_LIB=variants/$v.so timeout -k 10 200 python bench.py --steps 50 --warmup 10 --skip-cpu --skip-e2e --skip-u1 --skip-config3 --skip-u4 --skip-batched > gpurun_out/ab_$v.$rep.log 2>&1 || exit $?
     python - "$v" "$rep" <<'PY'
 import json, sys
 l = [x for x in open(f"gpurun_out/ab_{sys.argv[1]}.{sys.argv[2]}.log") if x.startswith("{")][-1]

@@ -1,7 +1,8 @@
 """Debug: phase stamps (s_memrealtime, 100 MHz) of k_refine_solve's blocks in
 one traced v3 call after warm-up calls -- entry, argmax done, votes done,
-partials reduced, ticket taken, last block's partials summed, solve done --
-relative to the first block's entry.  Needs a PVV_TRACE build:
+partials reduced, partial published, (the image's gathering block) all
+partials gathered and summed, solved; and when the block's pixels had
+arrived -- relative to the first block's entry.  Needs a PVV_TRACE build:
     python tools/build_variant.py trace -DPVV_TRACE
     PVVOTE_LIB=variants/trace.so python tools/refine_trace.py
 GPU only; not part of the product or the tests."""
@@ -22,7 +23,7 @@ seg = torch.from_numpy(f["seg"]).cuda()
 vert = torch.from_numpy(f["vertex"]).cuda()
 ws = VotingWorkspace()
 buf = torch.zeros(4096 * 8, dtype=torch.int64, device="cuda")
-names = ["entry", "argmax", "votes", "reduced", "ticket", "summed", "solved"]
+names = ["entry", "argmax", "votes", "reduced", "published", "gathered", "solved", "pixels"]
 res = []
 for trial in range(5):
     L.pv_debug_set_refine_trace(None)
