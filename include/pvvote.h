@@ -274,6 +274,11 @@ int pv_relu_maxpool_f32(const void *x, const void *bias, void *x2s, void *pool, 
  * add and relu; the sum's order differs from MIOpen's). */
 int pv_stem_conv_f16(const void *img, const void *w, const void *bias, void *out, int32_t n, int32_t h, int32_t wd,
                      pv_stream_t stream);
+/* the same convolution and, from the same pass, the maxpool after it (lib/networks/resnet.py:204:
+ * 3x3 / stride 2 / pad 1): x2s as above, pool [n][(h/2 - 1)/2 + 1][(wd/2 - 1)/2 + 1][64] (16-byte
+ * aligned) = max over each window of x2s (bit-equal to max_pool2d of x2s). */
+int pv_stem_pool_f16(const void *img, const void *w, const void *bias, void *x2s, void *pool, int32_t n, int32_t h,
+                     int32_t wd, pv_stream_t stream);
 
 /* replaces, for layer1's convolutions (lib/networks/resnet.py:21-70 BasicBlock conv1 / conv2 at
  * 64 -> 64 channels, 3x3, stride 1, pad 1), MIOpen's convolution + the epilogue pass after it:

@@ -2490,27 +2490,40 @@ extern "C" int pv_decoder_conv4s_f16(const void *fm, const void *skip, const voi
 
 
 // ==========================================================================
-// The stem's convolution (RN:139-142: conv1 7x7 / 2 / pad 3, 3 -> 64 channels,
-// BN folded, ReLU -> x2s) on the matrix cores.  A stride-2 7x7 convolution is
-// a stride-1 4x4 one over the image folded 2 x 2 into its channels
-// (space-to-depth): s2d pixel (Y, X) holds image pixels (2Y + dy, 2X + dx) as
-// channels dy*6 + dx*3 + c (12, padded to 16), and
+// The stem (RN:139-142, 201-204): conv1 7x7 / 2 / pad 3, 3 -> 64 channels,
+// BN folded, ReLU -> x2s, and maxpool 3x3 / 2 / pad 1 of x2s, on the matrix
+// cores, in one pass.  A stride-2 7x7 convolution is a stride-1 4x4 one over
+// the image folded 2 x 2 into its channels (space-to-depth): s2d pixel (Y, X)
+// holds image pixels (2Y + dy, 2X + dx) as channels dy*6 + dx*3 + c (12,
+// padded to 16), and
 //     x2s(y, x) = relu(b + sum_{ty,tx} W2[ty][tx] . s2d(y - 2 + ty, x - 2 + tx)),
 //     W2[ty][tx][dy*6 + dx*3 + c] = W[c][2ty + dy - 1][2tx + dx - 1]
 // (zero outside 0..6).  One tap = 16 channels = one v_mfma_f32_32x32x16_f16
 // per 32 output channels: 32 per wave and tile.  In the image's channels-last
 // fp16 layout the 6 channels of an s2d pixel's row dy are 12 contiguous bytes,
 // so a pixel is two 12-byte loads.
-// Persistent blocks of 8 waves (wave = output row, 32 pixels x 64 channels);
-// an 8 x 32 output tile reads an 11 x 35 s2d halo (12.3 KB in LDS, double
-// buffered; its two 16-byte granules per pixel swapped on odd 8-pixel groups:
-// conflict-free); halo pixels are loaded into registers two tiles ahead; the
-// weights (32 KB) stay in registers for the launch.  Epilogue: fp16 round,
-// + b, ReLU (as k_relu_pool), through LDS to 16-byte stores (a wave's output
-// row is 4 KB contiguous).  The maxpool after it is pv_relu_maxpool_f16's
-// pool-only form.
+// Tiles: 8 x2s rows (wave = row) x 32 computed columns x0 - 1 .. x0 + 30, of
+// which 30 are the tile's own (x0 = 30 tc): pool columns 15 tc .. 15 tc + 14
+// need x2s columns x0 - 1 .. x0 + 29, so the left neighbour column is
+// computed again (and the 32nd is computed unused) -- 7 % more matrix work
+// than 32-column tiles, for no halo exchange between tiles of a row.  Pool
+// rows 4 tr .. 4 tr + 3 need x2s rows y0 - 1 .. y0 + 7: row y0 - 1 is the
+// previous tile's last row, kept in LDS (two output buffers, alternating),
+// so tiles run top to bottom through a column strip: tile index = (image,
+// strip, row tile), row tile fastest, and a block takes a contiguous range
+// (when its range starts below a strip's top it first computes the tile
+// above, keeping only that row).  The pool's padding is 0, not -inf: x2s is a
+// ReLU output (>= 0, never NaN) and every window holds a valid pixel, so the
+// max is the same.  An 8 x 32 tile reads an 11 x 35 s2d halo (12.3 KB in
+// LDS, double buffered; its two 16-byte granules per pixel swapped on odd
+// 8-pixel groups: conflict-free); halo pixels are loaded into registers two
+// tiles ahead; the weights (32 KB) stay in registers for the launch.
+// Epilogue: fp16 round, + b, ReLU (as k_relu_pool), through LDS to 16-byte
+// x2s stores; one barrier, then the pool (one 8-channel output per thread,
+// 9 LDS reads, v_pk_max_f16) to 16-byte stores.  pool NULL: x2s only.
 // ==========================================================================
-constexpr int kSR = 8, kSC = 32;                      // output tile
+constexpr int kSR = 8, kSC = 32;                      // tile: 8 rows x 32 computed columns
+constexpr int kSNew = 30;                             // ... of which the tile's own (pool-aligned)
 constexpr int kSHR = kSR + 3, kSHC = kSC + 3;         // s2d halo: 11 x 35
 constexpr int kSHalo = kSHR * kSHC;                   // 385 pixels
 constexpr int kSCo = 64;
@@ -2521,32 +2534,37 @@ struct StemArgs {
     const _Float16 *w;      // [2 cout halves][16 taps][2 k halves][32 couts][8]: the lanes' A fragments
     const _Float16 *bias;   // [64]
     _Float16 *out;          // [N][H/2][W/2][64]
-    int N, H, W, Ho, Wo, tiles_r, tiles_c, ntiles;
+    _Float16 *pool;         // [N][Hp][Wp][64] or NULL
+    int N, H, W, Ho, Wo, Hp, Wp, tiles_r, tiles_c, ntiles;
 };
 
 __device__ __forceinline__ int stem_slot(int hp, int g) { return hp * 2 + (g ^ ((hp >> 3) & 1)); }
 
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_stem(StemArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t halo2[2][kSHalo * 32];
-    __shared__ __attribute__((aligned(16))) uint8_t obuf[8][kSC * kSCo * 2];   // each wave's 32 x 64 outputs
+    __shared__ __attribute__((aligned(16))) uint8_t obuf[2][kSR][kSC * kSCo * 2];   // two tiles' 8 x 32 x 64 outputs
     const int t = (int)threadIdx.x, lane = t & 63, wid = t >> 6;
     const int n = lane & 31, h = lane >> 5;
+    // this block's tiles: a contiguous range of (image, strip, row tile)
+    const int G = (int)gridDim.x, per = a.ntiles / G, rem = a.ntiles % G, bi = (int)blockIdx.x;
+    const int t0 = bi * per + min(bi, rem), t1 = t0 + per + (bi < rem ? 1 : 0);
+    if (t0 >= t1) return;
     h8 wf[2][16];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int tap = 0; tap < 16; ++tap) wf[m][tap] = *(const h8 *)(a.w + (((m * 16 + tap) * 2 + h) * 32 + n) * 8);
-    h4 bq[2][4];
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) bq[m][g] = *(const h4 *)(a.bias + 32 * m + 8 * g + 4 * h);
+    // the bias in LDS, read by the epilogue (registers are full: weights, halo
+    // addresses, two prefetch sets)
+    __shared__ _Float16 sbias[kSCo];
+    if (t < kSCo) sbias[t] = a.bias[t];
     __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0): no weight waits inside the tile loop
-    auto coords = [&](int tile, int &b, int &y0, int &x0) {
-        const int tc = tile % a.tiles_c, rest = tile / a.tiles_c;
-        b = rest / a.tiles_r;
-        y0 = (rest % a.tiles_r) * kSR;
-        x0 = tc * kSC;
+    auto coords = [&](int tile, int &b, int &tr, int &y0, int &x0) {
+        tr = tile % a.tiles_r;
+        const int rest = tile / a.tiles_r;
+        b = rest / a.tiles_c;
+        y0 = tr * kSR;
+        x0 = (rest % a.tiles_c) * kSNew;
     };
     // this thread's halo pixel (t < 385): rows 2Y and 2Y + 1, 12 bytes each;
     // two tiles ahead (a tile's MFMAs are shorter than a load's latency), in
@@ -2556,12 +2574,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // (issued for every tile, past the last as well -- with no access -- so the
     // count of loads in flight is the same on every path)
     auto fetch = [&](int tile, u3 &r0, u3 &r1) {
-        int b, y0, x0;
-        coords(min(tile, a.ntiles - 1), b, y0, x0);
+        int b, tr, y0, x0;
+        coords(min(tile, t1 - 1), b, tr, y0, x0);
         const __amdgpu_buffer_rsrc_t ir = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(a.img + (int64_t)b * a.H * a.W * 3), 0, a.H * a.W * 6, 0x00020000);
-        const int Y = y0 - 2 + hy, X = x0 - 2 + hx;
-        const bool ok = tile < a.ntiles && t < kSHalo && Y >= 0 && 2 * Y < a.H && X >= 0 && 2 * X < a.W;
+        // computed column c of the tile is x2s column x0 - 1 + c: s2d columns x0 - 3 + hx
+        const int Y = y0 - 2 + hy, X = x0 - 3 + hx;
+        const bool ok = tile < t1 && t < kSHalo && Y >= 0 && 2 * Y < a.H && X >= 0 && 2 * X < a.W;
         const uint32_t off = ok ? (uint32_t)((2 * Y * a.W + 2 * X) * 6) : 0x80000000u;
         const uint32_t off1 = ok ? off + (uint32_t)(a.W * 6) : 0x80000000u;
         r0 = __builtin_bit_cast(u3, __builtin_amdgcn_raw_buffer_load_b96(ir, off, 0, 0));
@@ -2573,37 +2592,47 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             *(u4 *)(halo + stem_slot(t, 1) * 16) = u4{r1.y, r1.z, 0u, 0u};
         }
     };
-    const int G = (int)gridDim.x;
-    uint8_t *ob = obuf[wid];
+    const __amdgpu_buffer_rsrc_t prr = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)a.pool, 0, a.pool ? 0x7fffffff : 0, 0x00020000);
     // Tile i: tile i + 2's loads, tile i's MFMAs, tile i + 1's halo into the
     // other buffer (its loads issued a tile earlier), tile i's outputs through
-    // LDS to 16-byte stores (a wave's output row is 4 KB contiguous), one
-    // barrier.
-    auto step = [&](int tile, const uint8_t *halo, uint8_t *next, u3 &f0, u3 &f1, const u3 &p0, const u3 &p1) {
-        int b, y0, x0;
-        coords(tile, b, y0, x0);
+    // LDS to 16-byte x2s stores, a barrier, the pool from this tile's rows and
+    // the previous tile's last.  `keep`: the tile above the range, computed
+    // for its last row only (no stores).
+    auto step = [&](int tile, const uint8_t *halo, uint8_t *next, u3 &f0, u3 &f1, const u3 &p0, const u3 &p1,
+                    uint8_t (*cur)[kSC * kSCo * 2], uint8_t (*prev)[kSC * kSCo * 2]) {
+        int b, tr, y0, x0;
+        coords(tile, b, tr, y0, x0);
+        const bool keep = tile < t0;
         __syncthreads();                      // this halo written; the reads of the other done
-        fetch(tile + 2 * G, f0, f1);
+        fetch(tile + 2, f0, f1);
         f16x acc0 = {}, acc1 = {};
+        // (the halo base through an opaque zero: the 16 per-tap offsets are then
+        // shared by both halo buffers instead of hoisted once for each)
+        int zh;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(zh));
+        const uint8_t *hb = halo + zh;
 #pragma unroll
         for (int tap = 0; tap < 16; ++tap) {
             const int ty = tap >> 2, tx = tap & 3;
-            const h8 bf = *(const h8 *)(halo + stem_slot((wid + ty) * kSHC + n + tx, h) * 16);
+            const h8 bf = *(const h8 *)(hb + stem_slot((wid + ty) * kSHC + n + tx, h) * 16);
             acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[0][tap], bf, acc0, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[1][tap], bf, acc1, 0, 0, 0);
         }
-        if (tile + G < a.ntiles) put(next, p0, p1);
+        if (tile + 1 < t1) put(next, p0, p1);
         // rows (i & 3) + 8 (i >> 2) + 4 h of acc = channels, column n = pixel:
-        // 8-byte pieces into the wave's LDS rows (16-byte chunk c of pixel n at
+        // 8-byte pieces into the wave's LDS row (16-byte chunk c of pixel n at
         // c ^ (n & 7): conflict-free both ways), read back as 16 bytes per lane
+        uint8_t *ob = cur[wid];
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 h4 y;
+                const h4 bq = *(const h4 *)(sbias + 32 * m + 8 * g + 4 * h);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const _Float16 v = (_Float16)((float)(_Float16)(m ? acc1 : acc0)[4 * g + j] + (float)bq[m][g][j]);
+                    const _Float16 v = (_Float16)((float)(_Float16)(m ? acc1 : acc0)[4 * g + j] + (float)bq[j]);
                     y[j] = (float)v > 0.f ? v : (_Float16)0.f;
                 }
                 *(h4 *)(ob + n * 128 + (((4 * m + g) ^ (n & 7)) * 16) + 8 * h) = y;
@@ -2614,45 +2643,88 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             (void *)(a.out + (int64_t)b * a.Ho * a.Wo * kSCo), 0, a.Ho * a.Wo * kSCo * 2, 0x00020000);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int p = 8 * r + (lane >> 3), q = lane & 7, ox = x0 + p;
+            const int p = 8 * r + (lane >> 3), q = lane & 7, ox = x0 - 1 + p;   // computed column p
             const u4 v = *(const u4 *)(ob + p * 128 + ((q ^ (p & 7)) * 16));
-            const uint32_t po = oy < a.Ho && ox < a.Wo ? (uint32_t)(((oy * a.Wo + ox) * kSCo) * 2 + q * 16) : 0x80000000u;
+            const bool own = !keep && p >= 1 && p <= kSNew && oy < a.Ho && ox < a.Wo;
+            const uint32_t po = own ? (uint32_t)(((oy * a.Wo + ox) * kSCo) * 2 + q * 16) : 0x80000000u;
             __builtin_amdgcn_raw_buffer_store_b128(v, orr, po, 0, 0);
         }
+        __syncthreads();                      // every row of this tile in LDS
+        // pool output (py, px), channels 8q .. 8q + 7: x2s rows 2py - 1 .. 2py + 1 =
+        // this tile's rows 2j - 1 .. 2j + 1 (row -1: the previous tile's row 7),
+        // computed columns 2i .. 2i + 2.  Waves 2j and 2j + 1 take pool row j
+        // (row addresses wave-uniform), lane pairs of waves the 120 (i, q)
+        {
+            // (the lane index through an opaque copy: everything below is made
+            // here, not hoisted out of the tile loop -- the registers are full)
+            int ol;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(ol) : "v"(lane));
+            const int j = wid >> 1, e = (wid & 1) * 64 + ol, i = e >> 3, q = e & 7;
+            const int py = (y0 >> 1) + j, px = (x0 >> 1) + i;
+            // x2s is >= +0 and never NaN: its fp16 bit patterns order as
+            // unsigned integers, so the max is v_pk_max_u16 on the bits
+            typedef unsigned short us8 __attribute__((ext_vector_type(8)));
+            us8 mx = {};
+            if (e < (kSNew / 2) * 8) {
+#pragma unroll
+                for (int dr = -1; dr <= 1; ++dr) {
+                    const int lr = 2 * j + dr, yy = y0 + lr;
+                    if (yy < 0 || yy >= a.Ho) continue;
+                    const uint8_t *row = lr < 0 ? prev[kSR - 1] : cur[lr];
+#pragma unroll
+                    for (int dc = 0; dc < 3; ++dc) {
+                        const int c = 2 * i + dc, xx = x0 - 1 + c;
+                        if (xx < 0 || xx >= a.Wo) continue;
+                        const us8 v = *(const us8 *)(row + (c * 128 + ((q ^ (c & 7)) * 16)));
+                        mx = __builtin_elementwise_max(mx, v);
+                    }
+                }
+            }
+            const bool own = !keep && e < (kSNew / 2) * 8 && py < a.Hp && px < a.Wp;
+            const uint32_t po = own ? ((uint32_t)((b * a.Hp + py) * a.Wp + px) * kSCo) * 2u + (uint32_t)q * 16u
+                                    : 0x80000000u;   // (< 2^31: checked at launch)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, mx), prr, po, 0, 0);
+        }
     };
-    int tile = (int)blockIdx.x;
-    if (tile >= a.ntiles) return;
-    fetch(tile, a0, a1);
-    fetch(tile + G, b0, b1);
-    {   // four dropped stores (out-of-range offset), as a step ends with: the
+    // the tile above the range's first, when that is not a strip's top: its last
+    // row is the first pool rows' row y0 - 1
+    const int first = (t0 % a.tiles_r) > 0 ? t0 - 1 : t0;
+    fetch(first, a0, a1);
+    fetch(first + 1, b0, b1);
+    {   // five dropped stores (out-of-range offset), as a step ends with: the
         // loop is entered with the same memory operations in flight as it
         // repeats with, so the compiler's wait before the first put() is for
-        // that tile's loads only (vmcnt(6)), not for the last stores as well
+        // that tile's loads only, not for the last stores as well
         const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc((void *)a.out, 0, 0, 0x00020000);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) __builtin_amdgcn_raw_buffer_store_b128(u4{0u, 0u, 0u, 0u}, orr, 0x80000000u + 16u * r, 0, 0);
+        for (int r = 0; r < 5; ++r) __builtin_amdgcn_raw_buffer_store_b128(u4{0u, 0u, 0u, 0u}, orr, 0x80000000u + 16u * r, 0, 0);
     }
     put(halo2[0], a0, a1);
+    int tile = first;
     while (true) {
-        step(tile, halo2[0], halo2[1], a0, a1, b0, b1);
-        if ((tile += G) >= a.ntiles) break;
-        step(tile, halo2[1], halo2[0], b0, b1, a0, a1);
-        if ((tile += G) >= a.ntiles) break;
+        step(tile, halo2[0], halo2[1], a0, a1, b0, b1, obuf[0], obuf[1]);
+        if (++tile >= t1) break;
+        step(tile, halo2[1], halo2[0], b0, b1, a0, a1, obuf[1], obuf[0]);
+        if (++tile >= t1) break;
     }
 }
 
-extern "C" int pv_stem_conv_f16(const void *img, const void *w, const void *bias, void *out, int32_t n, int32_t h,
-                                int32_t wd, pv_stream_t stream) {
+static int stem_launch(const void *img, const void *w, const void *bias, void *out, void *pool, int32_t n, int32_t h,
+                       int32_t wd, pv_stream_t stream) {
     if (!img || !w || !bias || !out || n < 0 || h < 2 || wd < 2 || h % 2 || wd % 2) return PV_EINVAL;
-    if (((uintptr_t)w | (uintptr_t)out) % 16 || (uintptr_t)bias % 8 || (uintptr_t)img % 4) return PV_EALIGN;
+    if (((uintptr_t)w | (uintptr_t)out | (uintptr_t)pool) % 16 || (uintptr_t)bias % 8 || (uintptr_t)img % 4)
+        return PV_EALIGN;
+    if (out == pool) return PV_EINVAL;
     if (n == 0) return PV_OK;
     if ((int64_t)h * wd * 6 >= (1ll << 31) || (int64_t)h * wd * kSCo / 2 >= (1ll << 31)) return PV_EINVAL;
     StemArgs a;
     a.img = (const _Float16 *)img; a.w = (const _Float16 *)w; a.bias = (const _Float16 *)bias;
-    a.out = (_Float16 *)out;
+    a.out = (_Float16 *)out; a.pool = (_Float16 *)pool;
     a.N = n; a.H = h; a.W = wd; a.Ho = h / 2; a.Wo = wd / 2;
+    a.Hp = (a.Ho - 1) / 2 + 1; a.Wp = (a.Wo - 1) / 2 + 1;
+    if (pool && (int64_t)n * a.Hp * a.Wp * kSCo * 2 >= (1ll << 31)) return PV_EINVAL;
     a.tiles_r = (a.Ho + kSR - 1) / kSR;
-    a.tiles_c = (a.Wo + kSC - 1) / kSC;
+    a.tiles_c = (a.Wo + kSNew - 1) / kSNew;
     const int64_t nt = (int64_t)n * a.tiles_r * a.tiles_c;
     if (nt >= (1ll << 31)) return PV_EINVAL;
     a.ntiles = (int)nt;
@@ -2660,6 +2732,17 @@ extern "C" int pv_stem_conv_f16(const void *img, const void *w, const void *bias
     k_stem<<<(unsigned)grid, 512, 0, (hipStream_t)stream>>>(a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? PV_OK : (int)e;
+}
+
+extern "C" int pv_stem_conv_f16(const void *img, const void *w, const void *bias, void *out, int32_t n, int32_t h,
+                                int32_t wd, pv_stream_t stream) {
+    return stem_launch(img, w, bias, out, nullptr, n, h, wd, stream);
+}
+
+extern "C" int pv_stem_pool_f16(const void *img, const void *w, const void *bias, void *x2s, void *pool, int32_t n,
+                                int32_t h, int32_t wd, pv_stream_t stream) {
+    if (!pool) return PV_EINVAL;
+    return stem_launch(img, w, bias, x2s, pool, n, h, wd, stream);
 }
 
 extern "C" int pv_conv64_f16(const void *x, const void *w, const void *bias, const void *res, void *out, int32_t n,

@@ -303,11 +303,13 @@ def stem_weights(c: nn.Conv2d):
     return w2.contiguous().half(), b
 
 
-def stem_conv(img: torch.Tensor, weights) -> torch.Tensor:
+def stem_conv(img: torch.Tensor, weights, pool: bool = False):
     """relu(conv1(img) + b) (RN:139-142, 201-203; BN folded) as one fp16
     matrix-core pass (``pv_stem_conv_f16``): img [n, 3, h, w] channels_last
     float16 CUDA, h and w even; ``weights`` from :func:`stem_weights`.
-    Returns x2s [n, 64, h/2, w/2] channels_last."""
+    Returns x2s [n, 64, h/2, w/2] channels_last; with ``pool`` also
+    maxpool 3x3 / 2 / 1 of it (RN:204) from the same pass
+    (``pv_stem_pool_f16``): (x2s, pool)."""
     n, c, h, w = img.shape
     if img.dtype != torch.float16 or not img.is_cuda or c != 3:
         raise RuntimeError("stem_conv: a [n, 3, h, w] float16 CUDA image required")
@@ -316,8 +318,15 @@ def stem_conv(img: torch.Tensor, weights) -> torch.Tensor:
     wt, b = weights
     out = torch.empty((n, 64, h // 2, w // 2), dtype=img.dtype, device=img.device,
                       memory_format=torch.channels_last)
-    _dev_call("pv_stem_conv_f16", None, img, img.data_ptr(), wt.data_ptr(), b.data_ptr(), out.data_ptr(), n, h, w)
-    return out
+    if not pool:
+        _dev_call("pv_stem_conv_f16", None, img, img.data_ptr(), wt.data_ptr(), b.data_ptr(), out.data_ptr(), n, h, w)
+        return out
+    ho, wo = h // 2, w // 2
+    pl = torch.empty((n, 64, (ho - 1) // 2 + 1, (wo - 1) // 2 + 1), dtype=img.dtype, device=img.device,
+                     memory_format=torch.channels_last)
+    _dev_call("pv_stem_pool_f16", None, img, img.data_ptr(), wt.data_ptr(), b.data_ptr(), out.data_ptr(),
+              pl.data_ptr(), n, h, w)
+    return out, pl
 
 
 def conv64_eligible(c: nn.Conv2d) -> bool:
@@ -736,8 +745,11 @@ class PVNetInference(nn.Module):
             if getattr(self, "_stem_key", None) != key:     # the kernel's weight layout, made once
                 self._stem_w = stem_weights(r.conv1)
                 self._stem_key = key
-            x2s = stem_conv(x, self._stem_w)
-            y = maxpool(x2s) if pool3 else mp(x2s)
+            if pool3:                                  # conv1 + bn + relu + maxpool in one pass
+                x2s, y = stem_conv(x, self._stem_w, pool=True)
+            else:
+                x2s = stem_conv(x, self._stem_w)
+                y = mp(x2s)
         elif pool3:
             x2s, y = relu_maxpool(_conv(x, r.conv1), r.conv1.bias)
         else:

@@ -836,7 +836,7 @@ def test_stem_weight_layout():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("hw", [(480, 640), (38, 70)])
+@pytest.mark.parametrize("hw", [(480, 640), (38, 70), (34, 126), (18, 62)])
 def test_stem_conv_matches_torch(hw, device):
     """pv_stem_conv_f16 (conv1 7x7/2/3 + folded BN + ReLU = x2s, RN:139-142,
     201-203) against MIOpen's fp16 convolution + ATen's bias add and ReLU; then
@@ -873,6 +873,18 @@ def test_stem_conv_matches_torch(hw, device):
         e = B.round_step(y64, e)
     B.check(got, torch.relu(y64), e, f"stem conv {h}x{w}")
     assert pool.is_contiguous(memory_format=cl) and torch.equal(pool, F.max_pool2d(got, 3, 2, 1))
+    # the fused pass (conv + maxpool, pv_stem_pool_f16): the same x2s, bit for
+    # bit, and the pool equal to max_pool2d of it -- tiles of 30 x2s columns and
+    # 8 rows, ragged at the right and bottom edges, ranges starting mid-strip
+    for nb in (2, 3):
+        imgb = img if nb == 2 else torch.cat([img, img[:1].flip(3)]).contiguous(memory_format=cl)
+        with torch.no_grad():
+            x2, pl = stem_conv(imgb, stem_weights(c), pool=True)
+            x2_only = stem_conv(imgb, stem_weights(c))
+        torch.cuda.synchronize()
+        assert torch.equal(x2, x2_only), f"fused stem x2s {h}x{w} batch {nb}"
+        assert pl.is_contiguous(memory_format=cl) and torch.equal(pl, F.max_pool2d(x2_only, 3, 2, 1)), \
+            f"fused stem pool {h}x{w} batch {nb}"
 
 
 def test_conv64_weight_layout():
