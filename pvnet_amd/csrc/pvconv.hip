@@ -48,6 +48,9 @@
 #endif
 #ifndef PVC_DEC_AHEAD
 #define PVC_DEC_AHEAD 3     // k_dec_conv consumers: fragment reads this many k-steps ahead of their MFMAs
+#ifndef PVC_DEC_2ROW
+#define PVC_DEC_2ROW 0      // 1: 4 consumer waves of 2 output rows (measured slower: conv4s 191 vs 160 us, conv2s 315 vs 250)
+#endif
 #endif
 #ifndef PVC_L1_AHEAD
 #define PVC_L1_AHEAD 2      // halo kernels (k_conv64, k_dec_conv2s / 4s): fragment reads this many k-steps ahead of their MFMAs
@@ -1816,14 +1819,21 @@ __device__ __forceinline__ int halo32(int hp, int q) { return hp * 4 + (q ^ ((hp
 // build done, [7] producer patch writes done
 __device__ unsigned long long *g_dec_trace;
 #define PVD_STAMP(it, j, k)                                                                                 \
-    if (g_dec_trace && (it) < 4 && lane == 0 && (wid == 0 || wid == 8))                                    \
+    if (g_dec_trace && (it) < 4 && lane == 0 && (wid == 0 || wid == kDecCW))                                  \
         g_dec_trace[(((int64_t)blockIdx.x * 4 + (it)) * 6 + (j)) * 8 + (k)] = __builtin_amdgcn_s_memtime()
 #else
 #define PVD_STAMP(it, j, k)
 #endif
 
+// Consumer waves (PVC_DEC_2ROW): 4, each two output rows -- a weight fragment
+// read from LDS feeds both rows' MFMAs (half the weight reads of one row per
+// wave; LDS bandwidth, not the matrix cores, bounded the one-row form) -- one
+// per SIMD; or 8 of one row.  Producer waves: 8.
+constexpr int kDecCW = PVC_DEC_2ROW ? 4 : 8;           // consumer waves
+constexpr int kDecRows = kTR / kDecCW;                 // output rows per consumer wave
+constexpr int kDecThreads = (kDecCW + 8) * 64;
 template <int CO, int NUP>
-__global__ __launch_bounds__(1024) void k_dec_conv(DecConvArgs a) {
+__global__ __launch_bounds__(kDecThreads) void k_dec_conv(DecConvArgs a) {
     constexpr int C1 = 32 * NUP;                       // fm channels
     constexpr int P = NUP + 2;                         // parts per tile (even: buffer parity = part parity)
     constexpr int WB = 36 * CO * 16;                   // one part's weights in LDS
@@ -1838,8 +1848,8 @@ __global__ __launch_bounds__(1024) void k_dec_conv(DecConvArgs a) {
     uint8_t *const wbuf = lds, *const hbuf = lds + 2 * WB, *const pbuf = lds + 2 * WB + 2 * kXHaloB;
     const int t = (int)threadIdx.x, lane = t & 63, wid = t >> 6;
     const int n = lane & 31, h = lane >> 5;
-    const bool consumer = wid < 8;
-    const int pt = t - 512;                            // producer thread (0..511)
+    const bool consumer = wid < kDecCW;
+    const int pt = t - kDecCW * 64;                    // producer thread (0..511)
     const int G = (int)gridDim.x;
     auto coords = [&](int tile, int &b, int &y0, int &x0, int &ly0, int &lx0) {
         const int tc = tile % a.tiles_c, rest = tile / a.tiles_c;
@@ -1852,35 +1862,34 @@ __global__ __launch_bounds__(1024) void k_dec_conv(DecConvArgs a) {
     // ---- consumers: weights by LDS-DMA, MFMAs, epilogue ----
     const __amdgpu_buffer_rsrc_t wr =
         __builtin_amdgcn_make_buffer_rsrc((void *)a.w, 0, (P / 2) * 9 * 8 * CO * 16, 0x00020000);
-    auto dma_weights = [&](int part) {                 // consumer waves: pieces wid, wid + 8, ...
+    auto dma_weights = [&](int part) {                 // consumer waves: pieces wid, wid + kDecCW, ...
         uint8_t *dst = wbuf + (part & 1) * WB;
         const int p64 = part >> 1, q0 = (part & 1) * 4;
-        for (int i = wid; i < PIECES; i += 8) {
+        for (int i = wid; i < PIECES; i += kDecCW) {
             const int byte = i * 1024 + lane * 16;
             const int blk = byte / (CO * 16), within = byte - blk * (CO * 16);
             const int tap = blk >> 2, q = blk & 3;
             glds16(wr, dst + i * 1024, (uint32_t)(((p64 * 9 + tap) * 8 + q0 + q) * (CO * 16) + within), 0u);
         }
     };
-    h4 bq[MT][4];
-    if (consumer) {
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) bq[m][g] = *(const h4 *)(a.bias + 32 * m + 8 * g + 4 * h);
-    }
-    f16x acc[MT];
+    f16x acc[kDecRows][MT];
+    // k-step s (tap s >> 1, channel half s & 1 of the part): the weight
+    // fragments once, the halo fragment of each of the wave's rows; the
+    // summation order of every output is the one-row form's
     auto mfma_part = [&](int part) {
         const uint8_t *W = wbuf + (part & 1) * WB, *Hb = hbuf + (part & 1) * kXHaloB;
-        auto frag = [&](int s, h8 &bf, h8 (&af)[MT]) {
+        auto frag = [&](int s, h8 (&bf)[kDecRows], h8 (&af)[MT]) {
             const int o = 2 * s + h, tap = o >> 2, q = o & 3;
             const int ky = tap / 3, kx = tap - 3 * ky;
-            bf = *(const h8 *)(Hb + halo32((wid + ky) * kHC + n + kx, q) * 16);
+#pragma unroll
+            for (int r = 0; r < kDecRows; ++r)
+                bf[r] = *(const h8 *)(Hb + halo32((kDecRows * wid + r + ky) * kHC + n + kx, q) * 16);
 #pragma unroll
             for (int m = 0; m < MT; ++m) af[m] = *(const h8 *)(W + ((tap * 4 + q) * CO + 32 * m + n) * 16);
         };
-        constexpr int AH = PVC_DEC_AHEAD;
-        h8 fb[AH + 1], fa[AH + 1][MT];
+        // (two rows of conv4s' 64 couts: 64 accumulator registers; fragments 2 steps ahead)
+        constexpr int AH = kDecRows * MT > 2 ? 2 : PVC_DEC_AHEAD;
+        h8 fb[AH + 1][kDecRows], fa[AH + 1][MT];
 #pragma unroll
         for (int s = 0; s < AH; ++s) frag(s, fb[s], fa[s]);
 #pragma unroll
@@ -1888,13 +1897,18 @@ __global__ __launch_bounds__(1024) void k_dec_conv(DecConvArgs a) {
             if (s + AH < 18) frag(s + AH, fb[(s + AH) % (AH + 1)], fa[(s + AH) % (AH + 1)]);
             const int c = s % (AH + 1);
 #pragma unroll
-            for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[c][m], fb[c], acc[m], 0, 0, 0);
+            for (int r = 0; r < kDecRows; ++r)
+#pragma unroll
+                for (int m = 0; m < MT; ++m)
+                    acc[r][m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[c][m], fb[c][r], acc[r][m], 0, 0, 0);
         }
     };
     auto epilogue = [&](int tile) {
         int b, y0, x0, ly0, lx0;
         coords(tile, b, y0, x0, ly0, lx0);
-        const int oy = y0 + wid, ox = x0 + n;
+#pragma unroll
+        for (int r = 0; r < kDecRows; ++r) {
+        const int oy = y0 + kDecRows * wid + r, ox = x0 + n;
         if (oy < a.H && ox < a.W) {
             _Float16 *op = a.out + (((int64_t)b * a.H + oy) * a.W + ox) * CO;
 #pragma unroll
@@ -1903,13 +1917,14 @@ __global__ __launch_bounds__(1024) void k_dec_conv(DecConvArgs a) {
                 for (int g = 0; g < 4; ++g) {
                     h4 y;
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) y[j] = (_Float16)acc[m][4 * g + j];
-                    y = y + bq[m][g];
+                    for (int j = 0; j < 4; ++j) y[j] = (_Float16)acc[r][m][4 * g + j];
+                    y = y + *(const h4 *)(a.bias + 32 * m + 8 * g + 4 * h);   // (cached; not held in registers)
                     h4 ys;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) ys[j] = (_Float16)((float)y[j] * a.slope);
                     *(h4 *)(op + 32 * m + 8 * g + 4 * h) = __builtin_elementwise_max(y, ys);
                 }
+        }
         }
     };
     // ---- producers: loads into registers, patch writes, halo builds ----
@@ -2036,7 +2051,9 @@ __global__ __launch_bounds__(1024) void k_dec_conv(DecConvArgs a) {
             (void)it;
             const bool more = tile + G < a.ntiles;
 #pragma unroll
-            for (int m = 0; m < MT; ++m) acc[m] = f16x{};
+            for (int r = 0; r < kDecRows; ++r)
+#pragma unroll
+                for (int m = 0; m < MT; ++m) acc[r][m] = f16x{};
 #pragma unroll 1     // (unrolled, the phases' fragment and DMA registers overlap: spills at MT = 2)
             for (int j = 0; j < P; ++j) {
                 PVD_STAMP(it, j, 0);
@@ -2446,7 +2463,7 @@ extern "C" int pv_decoder_conv2s_f16(const void *fm, const void *skip, const voi
 #if PVC_DEC_V1
     k_dec_conv2s<<<(unsigned)grid, 512, 0, (hipStream_t)stream>>>(a);
 #else
-    k_dec_conv<32, 2><<<(unsigned)grid, 1024, 0, (hipStream_t)stream>>>(a);
+    k_dec_conv<32, 2><<<(unsigned)grid, kDecThreads, 0, (hipStream_t)stream>>>(a);
 #endif
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? PV_OK : (int)e;
@@ -2482,7 +2499,7 @@ extern "C" int pv_decoder_conv4s_f16(const void *fm, const void *skip, const voi
 #if PVC_DEC_V1
     k_dec_conv4s<<<(unsigned)grid, 512, 0, (hipStream_t)stream>>>(a);
 #else
-    k_dec_conv<64, 4><<<(unsigned)grid, 1024, 0, (hipStream_t)stream>>>(a);
+    k_dec_conv<64, 4><<<(unsigned)grid, kDecThreads, 0, (hipStream_t)stream>>>(a);
 #endif
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? PV_OK : (int)e;
@@ -2519,11 +2536,25 @@ extern "C" int pv_decoder_conv4s_f16(const void *fm, const void *skip, const voi
 // 8-pixel groups: conflict-free); halo pixels are loaded into registers two
 // tiles ahead; the weights (32 KB) stay in registers for the launch.
 // Epilogue: fp16 round, + b, ReLU (as k_relu_pool), through LDS to 16-byte
-// x2s stores; one barrier, then the pool (one 8-channel output per thread,
-// 9 LDS reads, v_pk_max_f16) to 16-byte stores.  pool NULL: x2s only.
+// x2s stores.  A tile's pool runs one tile later, between the next tile's
+// barrier and its MFMAs (one 8-channel output per thread, its 9 LDS reads in
+// flight together, v_pk_max_u16 on the bits), to 16-byte stores: no barrier
+// of its own.  pool NULL: x2s only.  (tools/stem_probe.py, configs[2]'s
+// shape, one box, two rounds: conv + separate pool pass 228-232 us, this
+// kernel 137-140 us; with a barrier before the pool 143 us, with the pool's
+// reads one at a time 146-150 us, its 32-column form without the pool 108 us.)
 // ==========================================================================
+#ifndef PVC_STEM_ZH
+#define PVC_STEM_ZH 1
+#endif
+#ifndef PVC_STEM_POOLPOS
+#define PVC_STEM_POOLPOS 0  // where a tile's step runs the previous tile's pool: 0 before its MFMAs, 1 at its end (2: none, timing only)
+#endif
 constexpr int kSR = 8, kSC = 32;                      // tile: 8 rows x 32 computed columns
-constexpr int kSNew = 30;                             // ... of which the tile's own (pool-aligned)
+#ifndef PVC_STEM_NEW
+#define PVC_STEM_NEW 30     // (32: a timing diagnostic only -- the pool and the last column are then wrong)
+#endif
+constexpr int kSNew = PVC_STEM_NEW;                   // ... of which the tile's own (pool-aligned)
 constexpr int kSHR = kSR + 3, kSHC = kSC + 3;         // s2d halo: 11 x 35
 constexpr int kSHalo = kSHR * kSHC;                   // 385 pixels
 constexpr int kSCo = 64;
@@ -2543,6 +2574,8 @@ __device__ __forceinline__ int stem_slot(int hp, int g) { return hp * 2 + (g ^ (
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_stem(StemArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t halo2[2][kSHalo * 32];
     __shared__ __attribute__((aligned(16))) uint8_t obuf[2][kSR][kSC * kSCo * 2];   // two tiles' 8 x 32 x 64 outputs
+    __shared__ __attribute__((aligned(16))) uint8_t carry[3][kSC * kSCo * 2];        // three tiles' last rows
+    __shared__ __attribute__((aligned(16))) uint8_t zchunk[16];                       // zeros: the pool's padding
     const int t = (int)threadIdx.x, lane = t & 63, wid = t >> 6;
     const int n = lane & 31, h = lane >> 5;
     // this block's tiles: a contiguous range of (image, strip, row tile)
@@ -2558,8 +2591,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // addresses, two prefetch sets)
     __shared__ _Float16 sbias[kSCo];
     if (t < kSCo) sbias[t] = a.bias[t];
+    if (t < 4) ((uint32_t *)zchunk)[t] = 0u;
     __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0): no weight waits inside the tile loop
     auto coords = [&](int tile, int &b, int &tr, int &y0, int &x0) {
+#ifdef PVC_STEM_DIAG_ORDER   // timing diagnostic only (the pool is wrong): blocks' k-th tiles side by side
+        if (tile < per * G) tile = (tile % per) * G + tile / per;
+#endif
         tr = tile % a.tiles_r;
         const int rest = tile / a.tiles_r;
         b = rest / a.tiles_c;
@@ -2594,11 +2631,58 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     };
     const __amdgpu_buffer_rsrc_t prr = __builtin_amdgcn_make_buffer_rsrc(
         (void *)a.pool, 0, a.pool ? 0x7fffffff : 0, 0x00020000);
-    // Tile i: tile i + 2's loads, tile i's MFMAs, tile i + 1's halo into the
-    // other buffer (its loads issued a tile earlier), tile i's outputs through
-    // LDS to 16-byte x2s stores, a barrier, the pool from this tile's rows and
-    // the previous tile's last.  `keep`: the tile above the range, computed
-    // for its last row only (no stores).
+    // pool of tile `pt` (a tile of the range), run one tile behind, between the
+    // next tile's barrier and its MFMAs: its rows are `rows` (that tile's
+    // buffer, complete since the barrier), the row above is carry[(pt - 1) % 3]
+    // (the copy wave 7 made of the tile above's last row; three copies, so the
+    // one read here is not the one being written).  Output (py, px), channels
+    // 8q .. 8q + 7 = max over x2s rows 2py - 1 .. 2py + 1 = this tile's rows
+    // 2j - 1 .. 2j + 1, computed columns 2i .. 2i + 2; waves 2j and 2j + 1 take
+    // pool row j, their lanes the 120 (i, q).  Past the range (pt < t0 or
+    // pt >= t1) the store is dropped.
+    auto pool_tile = [&](int pt, uint8_t (*rows)[kSC * kSCo * 2], const uint8_t *above) {
+        int b, tr, y0, x0;
+        coords(max(pt, 0), b, tr, y0, x0);
+        // (the lane index through an opaque copy: everything below is made
+        // here, not hoisted out of the tile loop -- the registers are full)
+        int ol;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(ol) : "v"(lane));
+        const int j = wid >> 1, e = (wid & 1) * 64 + ol, i = e >> 3, q = e & 7;
+        const int py = (y0 >> 1) + j, px = (x0 >> 1) + i;
+        // x2s is >= +0 and never NaN: its fp16 bit patterns order as unsigned
+        // integers, so the max is v_pk_max_u16 on the bits
+        typedef unsigned short us8 __attribute__((ext_vector_type(8)));
+        // all nine reads in flight together (no branches: a window pixel
+        // outside the map reads the zero chunk instead), then the maxima.
+        // (Measured: the same work on waves 4-7 only, two outputs per lane, so
+        // that waves 0-3 start their MFMAs at once: 142-146 against 137-140 us.)
+        us8 v[9];
+#pragma unroll
+        for (int dr = 0; dr < 3; ++dr) {
+            const int lr = 2 * j + dr - 1, yy = y0 + lr;
+            const bool rok = yy >= 0 && yy < a.Ho;
+            const uint8_t *row = lr < 0 ? above : rows[lr < 0 ? 0 : lr];
+#pragma unroll
+            for (int dc = 0; dc < 3; ++dc) {
+                const int c = 2 * i + dc, xx = x0 - 1 + c;
+                const bool ok = rok && xx >= 0 && xx < a.Wo && e < (kSNew / 2) * 8;
+                v[dr * 3 + dc] = *(const us8 *)(ok ? row + (c * 128 + ((q ^ (c & 7)) * 16)) : zchunk);
+            }
+        }
+        us8 mx = v[0];
+#pragma unroll
+        for (int k = 1; k < 9; ++k) mx = __builtin_elementwise_max(mx, v[k]);
+        const bool own = pt >= t0 && pt < t1 && e < (kSNew / 2) * 8 && py < a.Hp && px < a.Wp;
+        const uint32_t po = own ? ((uint32_t)((b * a.Hp + py) * a.Wp + px) * kSCo) * 2u + (uint32_t)q * 16u
+                                : 0x80000000u;   // (< 2^31: checked at launch)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, mx), prr, po, 0, 0);
+    };
+    // Tile i: the barrier (tile i - 1's rows complete, this halo written), tile
+    // i + 2's loads, tile i - 1's pool, tile i's MFMAs, tile i + 1's halo into
+    // the other buffer (its loads issued a tile earlier), tile i's outputs
+    // through LDS to 16-byte x2s stores (wave 7 also keeps a copy of its row
+    // for tile i + 1's pool).  `keep`: the tile above the range, computed for
+    // its last row only (no stores).
     auto step = [&](int tile, const uint8_t *halo, uint8_t *next, u3 &f0, u3 &f1, const u3 &p0, const u3 &p1,
                     uint8_t (*cur)[kSC * kSCo * 2], uint8_t (*prev)[kSC * kSCo * 2]) {
         int b, tr, y0, x0;
@@ -2606,12 +2690,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         const bool keep = tile < t0;
         __syncthreads();                      // this halo written; the reads of the other done
         fetch(tile + 2, f0, f1);
+#if PVC_STEM_POOLPOS == 0
+        pool_tile(tile - 1, prev, carry[(tile + 1) % 3]);   // ((tile - 2) mod 3)
+#endif
         f16x acc0 = {}, acc1 = {};
         // (the halo base through an opaque zero: the 16 per-tap offsets are then
         // shared by both halo buffers instead of hoisted once for each)
+#if PVC_STEM_ZH
         int zh;
         asm volatile("v_mov_b32 %0, 0" : "=v"(zh));
         const uint8_t *hb = halo + zh;
+#else
+        const uint8_t *hb = halo;
+#endif
 #pragma unroll
         for (int tap = 0; tap < 16; ++tap) {
             const int ty = tap >> 2, tx = tap & 3;
@@ -2624,6 +2715,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         // 8-byte pieces into the wave's LDS row (16-byte chunk c of pixel n at
         // c ^ (n & 7): conflict-free both ways), read back as 16 bytes per lane
         uint8_t *ob = cur[wid];
+        uint8_t *cb = carry[tile % 3];
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -2635,7 +2727,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                     const _Float16 v = (_Float16)((float)(_Float16)(m ? acc1 : acc0)[4 * g + j] + (float)bq[j]);
                     y[j] = (float)v > 0.f ? v : (_Float16)0.f;
                 }
-                *(h4 *)(ob + n * 128 + (((4 * m + g) ^ (n & 7)) * 16) + 8 * h) = y;
+                const int off = n * 128 + (((4 * m + g) ^ (n & 7)) * 16) + 8 * h;
+                *(h4 *)(ob + off) = y;
+                if (wid == kSR - 1) *(h4 *)(cb + off) = y;
             }
         __builtin_amdgcn_wave_barrier();
         const int oy = y0 + wid;
@@ -2649,42 +2743,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             const uint32_t po = own ? (uint32_t)(((oy * a.Wo + ox) * kSCo) * 2 + q * 16) : 0x80000000u;
             __builtin_amdgcn_raw_buffer_store_b128(v, orr, po, 0, 0);
         }
-        __syncthreads();                      // every row of this tile in LDS
-        // pool output (py, px), channels 8q .. 8q + 7: x2s rows 2py - 1 .. 2py + 1 =
-        // this tile's rows 2j - 1 .. 2j + 1 (row -1: the previous tile's row 7),
-        // computed columns 2i .. 2i + 2.  Waves 2j and 2j + 1 take pool row j
-        // (row addresses wave-uniform), lane pairs of waves the 120 (i, q)
-        {
-            // (the lane index through an opaque copy: everything below is made
-            // here, not hoisted out of the tile loop -- the registers are full)
-            int ol;
-            asm volatile("v_mov_b32 %0, %1" : "=v"(ol) : "v"(lane));
-            const int j = wid >> 1, e = (wid & 1) * 64 + ol, i = e >> 3, q = e & 7;
-            const int py = (y0 >> 1) + j, px = (x0 >> 1) + i;
-            // x2s is >= +0 and never NaN: its fp16 bit patterns order as
-            // unsigned integers, so the max is v_pk_max_u16 on the bits
-            typedef unsigned short us8 __attribute__((ext_vector_type(8)));
-            us8 mx = {};
-            if (e < (kSNew / 2) * 8) {
-#pragma unroll
-                for (int dr = -1; dr <= 1; ++dr) {
-                    const int lr = 2 * j + dr, yy = y0 + lr;
-                    if (yy < 0 || yy >= a.Ho) continue;
-                    const uint8_t *row = lr < 0 ? prev[kSR - 1] : cur[lr];
-#pragma unroll
-                    for (int dc = 0; dc < 3; ++dc) {
-                        const int c = 2 * i + dc, xx = x0 - 1 + c;
-                        if (xx < 0 || xx >= a.Wo) continue;
-                        const us8 v = *(const us8 *)(row + (c * 128 + ((q ^ (c & 7)) * 16)));
-                        mx = __builtin_elementwise_max(mx, v);
-                    }
-                }
-            }
-            const bool own = !keep && e < (kSNew / 2) * 8 && py < a.Hp && px < a.Wp;
-            const uint32_t po = own ? ((uint32_t)((b * a.Hp + py) * a.Wp + px) * kSCo) * 2u + (uint32_t)q * 16u
-                                    : 0x80000000u;   // (< 2^31: checked at launch)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, mx), prr, po, 0, 0);
-        }
+#if PVC_STEM_POOLPOS == 1
+        pool_tile(tile - 1, prev, carry[(tile + 1) % 3]);   // ((tile - 2) mod 3)
+#endif
     };
     // the tile above the range's first, when that is not a strip's top: its last
     // row is the first pool rows' row y0 - 1
@@ -2707,6 +2768,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         step(tile, halo2[1], halo2[0], b0, b1, a0, a1, obuf[1], obuf[0]);
         if (++tile >= t1) break;
     }
+    // the last tile's pool: its rows are in obuf[(t1 - 1 - first) & 1]
+    __syncthreads();
+    pool_tile(t1 - 1, obuf[(t1 - 1 - first) & 1], carry[(t1 - 2 + 3) % 3]);
 }
 
 static int stem_launch(const void *img, const void *w, const void *bias, void *out, void *pool, int32_t n, int32_t h,
