@@ -1367,6 +1367,9 @@ __device__ __forceinline__ uint4 form_row(float ax, float ay, float b) {
     return make_uint4(pack_h2(axh, axh), pack_h2(axl, ayh), pack_h2(ayh, ayl), pack_h2(bh, bl));
 }
 
+#ifndef PVM_ALIGNED
+#define PVM_ALIGNED 1       // one image per launch: blocks aligned to (keypoint, group) segments
+#endif
 #ifndef PVM_WPE
 #define PVM_WPE 3   // 152 VGPRs, no spills (4: 128, spilled across the hot loop): 40.4k -> 41.5k images/s
 #endif
@@ -1394,8 +1397,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
     uint32_t total = 0;
     for (int b = 0; b < a.b; ++b) total += (uint32_t)(a.vn * ggn) * (uint32_t)tn_at(a, b);
     uint32_t lo, hi;
-    if (a.rw[0] > 0 && nunits % (a.rw[3] > 0 ? 4 : 3) == 0) round_share(total, nunits, (uint32_t)unit, a.rw, &lo, &hi);
-    else even_share(total, nunits, (uint32_t)unit, &lo, &hi);
+    const uint32_t nsegs = (uint32_t)(a.vn * ggn);
+    if (PVM_ALIGNED && a.b == 1 && a.rw[0] == 0 && nunits >= nsegs) {
+        // one image: every block inside one (keypoint, 512-hypothesis group)
+        // segment -- nunits / nsegs blocks per segment, the first nunits % nsegs
+        // segments one more -- so that no block pays a second segment's
+        // prologue (the launch's last waves were such blocks); the shares
+        // differ by at most one block's part of a segment (< 1 %)
+        const uint32_t base = nunits / nsegs, extra = nunits - base * nsegs;
+        uint32_t sg, k, nb;
+        if ((uint32_t)unit < extra * (base + 1)) {
+            sg = (uint32_t)unit / (base + 1); k = (uint32_t)unit - sg * (base + 1); nb = base + 1;
+        } else {
+            const uint32_t u2 = (uint32_t)unit - extra * (base + 1);
+            sg = extra + u2 / base; k = u2 - (u2 / base) * base; nb = base;
+        }
+        const uint64_t n = (uint64_t)tn_at(a, 0);
+        lo = sg * (uint32_t)n + (uint32_t)(k * n / nb);
+        hi = sg * (uint32_t)n + (uint32_t)((k + 1) * n / nb);
+    } else if (a.rw[0] > 0 && nunits % (a.rw[3] > 0 ? 4 : 3) == 0) {
+        round_share(total, nunits, (uint32_t)unit, a.rw, &lo, &hi);
+    } else {
+        even_share(total, nunits, (uint32_t)unit, &lo, &hi);
+    }
     int buf = 0, nfix = 0, nseg = 0, nslow = 0, nxo = 0;
     uint64_t tloop = 0, t_total = 0, t_hyp = 0;
     uint64_t c_stage = 0, c_hot = 0, c_fix = 0, c_seg = 0, c_mark = 0;   // debug: shader cycles per phase
