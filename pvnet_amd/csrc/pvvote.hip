@@ -1368,7 +1368,11 @@ __device__ __forceinline__ uint4 form_row(float ax, float ay, float b) {
 }
 
 #ifndef PVM_ALIGNED
-#define PVM_ALIGNED 1       // one image per launch: blocks aligned to (keypoint, group) segments
+// 1: one-image launches split along (keypoint, group) segments -- no block
+// pays a second segment's prologue: the launch alone 28.1 -> 25.4 us span
+// (tools/vote_trace.py), but sequential latency only 48.3-48.7 -> 48.0-48.2 us
+// and the stream 54.2k -> 53.3-53.6k images/s (tools/ab_libs.sh, two rounds)
+#define PVM_ALIGNED 0
 #endif
 #ifndef PVM_WPE
 #define PVM_WPE 3   // 152 VGPRs, no spills (4: 128, spilled across the hot loop): 40.4k -> 41.5k images/s
