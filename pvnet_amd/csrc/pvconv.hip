@@ -211,6 +211,9 @@ __device__ __forceinline__ ColW col_weights(const TailArgs &a, int c, int x0, in
 // (Measured: a branch-free form sharing a thread's four column blends over
 // its five rows, with bit-mask picks, was 6 % slower -- the picks cost more
 // VALU than the reads they save.)
+#ifndef PVT_BLEND4
+#define PVT_BLEND4 0        // 1: the tail's blend with one fp16 weight per source (backbone 4.949-4.960 vs 4.954-4.963 ms: no gain)
+#endif
 __device__ __forceinline__ void halo_blend(const TailArgs &a, const _Float16 *patch, _Float16 *halo, const ColW &w,
                                            int c, int hy, bool colok, int y0, int ly0) {
     const int oy = y0 - 1 + hy;
@@ -223,9 +226,19 @@ __device__ __forceinline__ void halo_blend(const TailArgs &a, const _Float16 *pa
         const _Float16 *p = patch + (h1 - ly0) * (kPC * 32) + w.poff;
         const h8 A = *(const h8 *)p, B = *(const h8 *)(p + w.dp);
         const h8 C = *(const h8 *)(p + dh), D = *(const h8 *)(p + dh + w.dp);
+#if PVT_BLEND4
+        // one weight per source (f32 products rounded once to fp16): 4 packed
+        // ops per 2 channels instead of the separable form's 6
+        const float cw0 = (float)w.w0, cw1 = (float)w.w1;
+        const _Float16 q00 = (_Float16)(cw0 * (1.f - h1l)), q01 = (_Float16)(cw1 * (1.f - h1l));
+        const _Float16 q10 = (_Float16)(cw0 * h1l), q11 = (_Float16)(cw1 * h1l);
+        v = __builtin_elementwise_fma(D, (h8)q11, __builtin_elementwise_fma(C, (h8)q10,
+                __builtin_elementwise_fma(B, (h8)q01, A * (h8)q00)));
+#else
         const h8 c0 = __builtin_elementwise_fma(B, (h8)w.w1, A * (h8)w.w0);
         const h8 c1 = __builtin_elementwise_fma(D, (h8)w.w1, C * (h8)w.w0);
         v = __builtin_elementwise_fma(c1, (h8)(_Float16)h1l, c0 * (h8)(_Float16)(1.f - h1l));
+#endif
     }
     *(h8 *)(halo + hy * (kHC * kCP) + (c >> 2) * kCP + 8 * (c & 3)) = v;
 }
