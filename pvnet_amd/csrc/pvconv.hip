@@ -48,9 +48,9 @@
 #endif
 #ifndef PVC_DEC_AHEAD
 #define PVC_DEC_AHEAD 3     // k_dec_conv consumers: fragment reads this many k-steps ahead of their MFMAs
+#endif
 #ifndef PVC_DEC_2ROW
 #define PVC_DEC_2ROW 0      // 1: 4 consumer waves of 2 output rows (measured slower: conv4s 191 vs 160 us, conv2s 315 vs 250)
-#endif
 #endif
 #ifndef PVC_L1_AHEAD
 #define PVC_L1_AHEAD 2      // halo kernels (k_conv64, k_dec_conv2s / 4s): fragment reads this many k-steps ahead of their MFMAs
