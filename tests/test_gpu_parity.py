@@ -354,6 +354,34 @@ def test_v3_refine_sums_match_oracle(case, thr_mode, device, rvg):
     np.testing.assert_allclose(diag["atb"][0].reshape(vn, 2), atb, rtol=1e-6, atol=1e-7 * np.abs(atb).max())
 
 
+def test_v3_many_hypotheses(device, rvg):
+    """round_hyp_num 2048 (> 1024: k_refine_solve's instantiation that keeps the
+    hypotheses in memory and reads the counts past the first 1024 in a loop)
+    on a cropped synthetic frame, against the oracle with the same pixel
+    pairs: counts bit-exact, the winners, the fp64 sums, the keypoints."""
+    g = G.load("synth_v3_512")
+    mask, vertex, _ = G.synth_inputs(g)
+    crop = np.zeros_like(mask)
+    crop[:, 190:250, 280:340] = mask[:, 190:250, 280:340]      # a few thousand foreground pixels
+    tn = int(O.fg_mask_v3(crop[0]).sum())
+    assert 1000 < tn < 4000
+    hn = 2048
+    idxs = np.random.default_rng(5).integers(0, tn, size=(1, hn, vertex.shape[3], 2), dtype=np.int32)
+    diag = {}
+    kp = rvg.ransac_voting_layer_v3(cu(crop, device), cu(vertex, device), hn, _idxs=idxs, _diag=diag).cpu().numpy()
+    diag = {k: v.cpu().numpy() for k, v in diag.items()}
+    dg = []
+    ko = O.ransac_voting_layer_v3(crop, vertex, hn, idxs=[idxs[0]], diag=dg)
+    np.testing.assert_array_equal(diag["counts"][0].T, dg[0]["counts"])
+    np.testing.assert_array_equal(diag["win_idx"][0], dg[0]["win_idx"])
+    vn = vertex.shape[3]
+    np.testing.assert_allclose(diag["ata"][0].reshape(vn, 2, 2), dg[0]["ATA"], rtol=1e-6,
+                               atol=1e-7 * np.abs(dg[0]["ATA"]).max())
+    np.testing.assert_allclose(diag["atb"][0].reshape(vn, 2), dg[0]["ATb"], rtol=1e-6,
+                               atol=1e-7 * np.abs(dg[0]["ATb"]).max())
+    np.testing.assert_allclose(kp, ko, atol=KP_TOL, rtol=0)
+
+
 def test_v3_from_network_fused(device, rvg):
     """seg_pred/vertex_pred straight from the network layout (argmax fused)."""
     g = G.load("synth_v3_512")
