@@ -273,9 +273,20 @@ __device__ __forceinline__ T ld_agent(const T *p) { return __hip_atomic_load(p, 
 // --------------------------------------------------------------------------
 // block helpers (256 threads = 4 waves)
 // --------------------------------------------------------------------------
+// wave sums (every lane gets the sum): DPP within each 16-lane row, then
+// v_permlane16_swap / v_permlane32_swap across rows -- no ds_bpermute round
+// trips (six serial LDS latencies in the __shfl_xor form)
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int x) { return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, true); }
 __device__ __forceinline__ int wave_sum_i(int x) {
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-    return x;
+    x += dpp_i<0xB1>(x);
+    x += dpp_i<0x4E>(x);
+    x += dpp_i<0x141>(x);
+    x += dpp_i<0x140>(x);
+    const auto r16 = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    x = (int)(r16[0] + r16[1]);
+    const auto r32 = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return (int)(r32[0] + r32[1]);
 }
 __device__ __forceinline__ double wave_sum_d(double x) {
     for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
@@ -1804,7 +1815,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
         int32_t *cp = a.counts + (int64_t)b * a.cnt_bs + (int64_t)v * a.cnt_v;
 #pragma unroll
         for (int j = 0; j < kMSet; ++j) {
-            const int tot = cnt[j] + __shfl_xor(cnt[j], 32);
+            const auto sw = __builtin_amdgcn_permlane32_swap(cnt[j], cnt[j], false, false);
+            const int tot = (int)(sw[0] + sw[1]);   // both halves, VALU only
             const int h = hg * kGroup + j * 32 + col;
             if (half == 0 && h < a.nh && tot) atomicAdd(&cp[(int64_t)h * a.cnt_h], tot);
         }
