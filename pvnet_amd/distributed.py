@@ -41,8 +41,8 @@ def gather_results(local: torch.Tensor, n_images: int, rank: int, world: int,
     """
     per = (n_images + world - 1) // world
     feat = tuple(local.shape[1:])
-    if world == 1:
-        return local
+    if world == 1 and not (dist.is_available() and dist.is_initialized()):
+        return local        # no process group: nothing to exchange (with one, the collective runs: a copy)
     if local.shape[0] != len(range(rank, n_images, world)):
         raise ValueError(f"rank {rank} holds {local.shape[0]} results, its shard has {len(range(rank, n_images, world))}")
     # RCCL moves device tensors over xGMI; gloo (the CPU tests, or ranks that

@@ -291,3 +291,41 @@ def test_config4_stream_two_ranks_gloo(device, tmp_path):
     for k in r0.files:
         np.testing.assert_array_equal(r0[k], r1[k])
     check_ycb_stream([torch.from_numpy(r0[f"arr_{k}"]) for k in range(3)])
+
+
+def _rccl_worker(rank, port, out_path):
+    """One rank over the nccl backend (RCCL on ROCm) with the device given at
+    init, as bench.py's multi-GPU ranks start: the stream's gather then runs
+    RCCL's all_gather_into_tensor on device tensors (a one-rank copy, but the
+    same backend, communicator setup and device-tensor path an 8-GPU run
+    takes; RCCL refuses two ranks on one device)."""
+    import torch.distributed as dist
+    from pvnet_amd import ransac_voting_gpu as rvg
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=rank, world_size=1, device_id=dev)
+    try:
+        assert dist.get_backend() == "nccl"
+        diags = {}
+        res = D.run_stream(make_load(dev), make_vote(rvg.VotingWorkspace(), diags), N_IMAGES, 0, 1, (9, 2), dev)
+        assert res.device == dev and res.shape == (N_IMAGES, 9, 2)
+        kp, cov = torch.randn(5, 9, 2, device=dev), torch.randn(5, 9, 2, 2, device=dev)
+        pose = torch.randn(5, 3, 4, device=dev, dtype=torch.float64)
+        g = D.gather_results_multi([kp, cov, pose], 5, 0, 1)
+        assert all(x.device == dev for x in g)
+        assert torch.equal(g[0], kp) and torch.equal(g[1], cov) and torch.equal(g[2], pose)
+        np.save(out_path + ".npy", res.cpu().numpy())
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_config3_stream_rccl_one_rank(device, tmp_path):
+    """The nccl (RCCL) backend's gather path on the device: every keypoint in
+    stream order, equal to the oracle's."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "rccl")
+    mp.spawn(_rccl_worker, args=(_free_port(), out), nprocs=1, join=True)
+    check_against_oracle(np.load(out + ".npy"), None)
