@@ -373,6 +373,14 @@ int pv_decoder_conv4s_f16(const void *fm, const void *skip, const void *w, const
 int pv_decoder_tail_f16(const void *fm, const void *img, const void *w1, const float *b1, const void *w2,
                         const float *b2, void *out, int32_t n, int32_t hin, int32_t win, int32_t cout, float slope,
                         pv_stream_t stream);
+/* pv_decoder_tail_f16 with the head's output split the way the network returns it (model_repository.py:79:
+ * seg_pred = x[:, :seg_dim], ver_pred = x[:, seg_dim:], seg_dim = 2): seg [n][2hin][2win][2] and ver
+ * [n][2hin][2win][cout - 2], each channels-last and dense, so the voting layer's argmax reads 4 bytes per
+ * pixel instead of the whole cout-channel record's cache lines.  The same values as pv_decoder_tail_f16's
+ * channels.  seg, ver 4-byte aligned. */
+int pv_decoder_tail_split_f16(const void *fm, const void *img, const void *w1, const float *b1, const void *w2,
+                              const float *b2, void *seg, void *ver, int32_t n, int32_t hin, int32_t win,
+                              int32_t cout, float slope, pv_stream_t stream);
 
 #ifdef __cplusplus
 }

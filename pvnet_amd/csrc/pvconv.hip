@@ -88,7 +88,8 @@ struct TailArgs {
     const float *b1;       // [32]
     const _Float16 *w2;    // [MT][2][32][16]: the 1x1 weights in the accumulator's row order (host-permuted)
     const float *b2;       // [cout]
-    _Float16 *out;         // [N][H][W][cout]
+    _Float16 *out;         // [N][H][W][cout]; split: the vertex channels [N][H][W][cout - 2]
+    _Float16 *seg;         // split: the two segmentation channels [N][H][W][2]; else null
     int N, Hin, Win, H, W, tiles_r, tiles_c, ntiles;
     float rh, rw, slope;
 #ifdef PVT_TRACE
@@ -257,6 +258,41 @@ __device__ __forceinline__ void halo_blend(const TailArgs &a, const _Float16 *pa
 #endif
 
 #if PVT_V1
+// The head's output stores: 4 channels o0 .. o0 + 3 of one pixel (8 bytes).
+// Unsplit, [N][H][W][cout] at 2 * (cout pix + o0).  Split (pv_decoder_tail_split_f16),
+// channels 0-1 go to seg [N][H][W][2] and the rest to the vertex map [N][H][W][cout - 2]:
+// group 0 is one 4-byte store to each, a later group one 8-byte store (4-byte
+// aligned) to the vertex map.  Buffer descriptors per image; pix < 0 (outside
+// the image) gives an offset past the range, so the store is dropped.
+struct TailOut {
+    __amdgpu_buffer_rsrc_t o, sg;
+    bool split;
+};
+template <int COUT>
+__device__ __forceinline__ TailOut tail_out(const TailArgs &a, int b) {
+    const int64_t hw = (int64_t)a.H * a.W;
+    TailOut t;
+    t.split = a.seg != nullptr;
+    const int oc = t.split ? COUT - 2 : COUT;
+    t.o = image_rsrc(a.out + b * hw * oc, hw * oc * 2);
+    t.sg = image_rsrc(t.split ? a.seg + b * hw * 2 : a.out, t.split ? hw * 4 : 0);
+    return t;
+}
+template <int COUT>
+__device__ __forceinline__ void tail_store(const TailOut &t, int pix, int o0, h4 v) {
+    const u2 w = __builtin_bit_cast(u2, v);
+    if (!t.split) {
+        const int po = pix >= 0 ? pix * (COUT * 2) + 2 * o0 : (int)0x80000000;
+        __builtin_amdgcn_raw_buffer_store_b64(w, t.o, po, 0, 0);
+    } else if (o0 == 0) {
+        __builtin_amdgcn_raw_buffer_store_b32(w.x, t.sg, pix >= 0 ? pix * 4 : (int)0x80000000, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(w.y, t.o, pix >= 0 ? pix * ((COUT - 2) * 2) : (int)0x80000000, 0, 0);
+    } else {
+        const int po = pix >= 0 ? pix * ((COUT - 2) * 2) + 2 * (o0 - 2) : (int)0x80000000;
+        __builtin_amdgcn_raw_buffer_store_b64(w, t.o, po, 0, 0);
+    }
+}
+
 template <int COUT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVT_WPE, PVT_WPE))) void k_decoder_tail(TailArgs a) {
     constexpr int MT = (COUT + 31) / 32;
@@ -367,8 +403,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVT_WPE, PV
 #endif
         PVT_STAMP(7);
         // ---- epilogue + head, per row ----
-        const __amdgpu_buffer_rsrc_t orr =
-            image_rsrc(a.out + (int64_t)b * a.H * a.W * COUT, (int64_t)a.H * a.W * COUT * 2);
+        const TailOut to = tail_out<COUT>(a, b);
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
             const int oy = y0 + 2 * wid + r, ox = x0 + n;
@@ -388,8 +423,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVT_WPE, PV
 #pragma unroll
                 for (int j = 0; j < 4; ++j) act[gq >> 1][4 * (gq & 1) + j] = y[j];
             }
-            // byte offset of the pixel's outputs; past the buffer (dropped) outside the image
-            const int po = (oy < a.H && ox < a.W) ? (oy * a.W + ox) * (COUT * 2) : (int)0x80000000;
+            // the pixel; -1 outside the image (its stores dropped)
+            const int pix = (oy < a.H && ox < a.W) ? oy * a.W + ox : -1;
 #pragma unroll
             for (int t = 0; t < MT; ++t) {
                 f16x d = {};
@@ -406,7 +441,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVT_WPE, PV
 #ifdef PVT_SKIP_STORE
                         if (v[0] == (_Float16)1234.5f)
 #endif
-                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), orr, po + 2 * o0, 0, 0);
+                        tail_store<COUT>(to, pix, o0, v);
                     }
                 }
             }
@@ -482,8 +517,7 @@ __global__ __launch_bounds__(512) void k_decoder_tail2(TailArgs a) {
                 acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa[s], fb[c][0], acc[0], 0, 0, 0);
                 acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa[s], fb[c][1], acc[1], 0, 0, 0);
             }
-            const __amdgpu_buffer_rsrc_t orr =
-                image_rsrc(a.out + (int64_t)b * a.H * a.W * COUT, (int64_t)a.H * a.W * COUT * 2);
+            const TailOut to = tail_out<COUT>(a, b);
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 const int oy = y0 + 2 * wid + r, ox = x0 + n;
@@ -502,7 +536,7 @@ __global__ __launch_bounds__(512) void k_decoder_tail2(TailArgs a) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) act[gq >> 1][4 * (gq & 1) + j] = y[j];
                 }
-                const int po = (oy < a.H && ox < a.W) ? (oy * a.W + ox) * (COUT * 2) : (int)0x80000000;
+                const int pix = (oy < a.H && ox < a.W) ? oy * a.W + ox : -1;
 #pragma unroll
                 for (int m = 0; m < MT; ++m) {
                     f16x d = {};
@@ -516,7 +550,7 @@ __global__ __launch_bounds__(512) void k_decoder_tail2(TailArgs a) {
 #pragma unroll
                             for (int j = 0; j < 4; ++j) v[j] = (_Float16)d[4 * q + j];
                             v = v + *(const h4 *)(bias + 32 + o0);
-                            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), orr, po + 2 * o0, 0, 0);
+                            tail_store<COUT>(to, pix, o0, v);
                         }
                     }
                 }
@@ -2276,16 +2310,17 @@ int cu_count_dec() {
 
 }  // namespace
 
-extern "C" int pv_decoder_tail_f16(const void *fm, const void *img, const void *w1, const float *b1, const void *w2,
-                                   const float *b2, void *out, int32_t n, int32_t hin, int32_t win, int32_t cout,
-                                   float slope, pv_stream_t stream) {
+static int decoder_tail(const void *fm, const void *img, const void *w1, const float *b1, const void *w2,
+                        const float *b2, void *out, void *seg, int32_t n, int32_t hin, int32_t win, int32_t cout,
+                        float slope, pv_stream_t stream) {
     if (!fm || !img || !w1 || !b1 || !w2 || !b2 || !out || n < 0 || hin < 2 || win < 2) return PV_EINVAL;
     if (cout != 20 && cout != 44) return PV_EINVAL;
     if (!(slope >= 0.f && slope < 1.f)) return PV_EINVAL;          // LeakyReLU as max(y, slope y)
-    if (((uintptr_t)fm | (uintptr_t)w1 | (uintptr_t)w2) % 16 || (uintptr_t)out % 8 || (uintptr_t)img % 4)
-        return PV_EALIGN;
+    if (((uintptr_t)fm | (uintptr_t)w1 | (uintptr_t)w2) % 16 || (uintptr_t)img % 4) return PV_EALIGN;
+    if (seg ? ((uintptr_t)out | (uintptr_t)seg) % 4 : (uintptr_t)out % 8) return PV_EALIGN;
     if (n == 0) return PV_OK;
     TailArgs a;
+    a.seg = (_Float16 *)seg;
     a.fm = (const _Float16 *)fm;
     a.img = (const _Float16 *)img;
     a.w1 = (const _Float16 *)w1;
@@ -2321,6 +2356,19 @@ extern "C" int pv_decoder_tail_f16(const void *fm, const void *img, const void *
 #endif
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? PV_OK : (int)e;
+}
+
+extern "C" int pv_decoder_tail_f16(const void *fm, const void *img, const void *w1, const float *b1, const void *w2,
+                                   const float *b2, void *out, int32_t n, int32_t hin, int32_t win, int32_t cout,
+                                   float slope, pv_stream_t stream) {
+    return decoder_tail(fm, img, w1, b1, w2, b2, out, nullptr, n, hin, win, cout, slope, stream);
+}
+
+extern "C" int pv_decoder_tail_split_f16(const void *fm, const void *img, const void *w1, const float *b1,
+                                         const void *w2, const float *b2, void *seg, void *ver, int32_t n, int32_t hin,
+                                         int32_t win, int32_t cout, float slope, pv_stream_t stream) {
+    if (!seg) return PV_EINVAL;
+    return decoder_tail(fm, img, w1, b1, w2, b2, ver, seg, n, hin, win, cout, slope, stream);
 }
 
 #ifdef PVT_TRACE

@@ -336,17 +336,21 @@ __device__ __forceinline__ int2 block_sum2(int x, int y, int *sh) {
 // ==========================================================================
 // K1: foreground count per 256-pixel chunk (one pixel per thread and chunk)
 // and the chunk's four wave ballots (k_compact reads 32 B instead of the mask
-// again); zeroes the pipeline's counters.  A block takes kFgCPB consecutive
-// chunks, their mask loads in flight together (tools/lat_ab.sh, two rounds:
-// 1 chunk 43.8-43.9k images/s and 52.1-52.4 us sequential latency, 2 chunks
-// 43.8k / 52.8-53.1 us, 4 chunks 43.6k / 54.3 us; the former block_sum2 form
-// with two barriers 43.5k / 52.6-52.8 us).
+// again); zeroes the pipeline's counters.  A block takes CPB consecutive
+// chunks, their mask loads issued together (clamped to the image, so no
+// branch sits between them).  One chunk per block for grids that fit the
+// chip at once (a one-image call: tools/lat_ab.sh, 1 chunk 52.1-52.4 us
+// sequential latency, 2 chunks 52.8-53.1, 4 chunks 54.3); kFgWideCPB for
+// larger grids, where one-chunk blocks -- one mask round trip each, eight
+// per CU at a time -- left the kernel bound by block turnover (configs[2],
+// 32 frames: 70 us).
 // ==========================================================================
-#ifndef PVV_FG_CPB
-#define PVV_FG_CPB 1
+#ifndef PVV_FG_WIDE_ABOVE
+#define PVV_FG_WIDE_ABOVE 4096
 #endif
-constexpr int kFgCPB = PVV_FG_CPB;
-template <int KIND, bool EVD>
+constexpr int kFgWideCPB = 8;
+constexpr int64_t kFgWideAbove = PVV_FG_WIDE_ABOVE;   // blocks of one chunk above which the wide form runs
+template <int KIND, bool EVD, int CPB>
 __global__ __launch_bounds__(256) void k_fg_count(MaskView m, int H, int W, int32_t *blkcnt, uint64_t *fgbits,
                                                   int nblk, int32_t *zero, int64_t zero_words) {
     static_assert(kCompactChunk == 256, "one pixel per thread");
@@ -357,17 +361,19 @@ __global__ __launch_bounds__(256) void k_fg_count(MaskView m, int H, int W, int3
         int64_t G = (int64_t)gridDim.x * gridDim.y * 256;
         for (int64_t i = g; i < zero_words; i += G) zero[i] = 0;
     }
-    __shared__ int sh[kFgCPB][4];
-    bool f[kFgCPB];
+    __shared__ int sh[CPB][4];
+    bool f[CPB];
 #pragma unroll
-    for (int k = 0; k < kFgCPB; ++k) {
-        const int blk = blockIdx.x * kFgCPB + k;
+    for (int k = 0; k < CPB; ++k) {
+        const int blk = blockIdx.x * CPB + k;
         const int64_t p = (int64_t)blk * kCompactChunk + threadIdx.x;
-        f[k] = blk < nblk && p < P && is_fg<KIND, EVD>(m, b, (int)((uint32_t)p / (uint32_t)W), (int)((uint32_t)p % (uint32_t)W));
+        const uint32_t pc = (uint32_t)min(p, P - 1);   // every load in range: none behind a branch
+        const bool v = is_fg<KIND, EVD>(m, b, (int)(pc / (uint32_t)W), (int)(pc % (uint32_t)W));
+        f[k] = blk < nblk && p < P && v;
     }
 #pragma unroll
-    for (int k = 0; k < kFgCPB; ++k) {
-        const int blk = blockIdx.x * kFgCPB + k;   // block-uniform
+    for (int k = 0; k < CPB; ++k) {
+        const int blk = blockIdx.x * CPB + k;   // block-uniform
         if (blk >= nblk) break;
         const uint64_t bal = ballot(f[k]);
         if (lane_id() == 0) {
@@ -376,8 +382,8 @@ __global__ __launch_bounds__(256) void k_fg_count(MaskView m, int H, int W, int3
         }
     }
     __syncthreads();
-    const int blk = blockIdx.x * kFgCPB + (int)threadIdx.x;
-    if (threadIdx.x < kFgCPB && blk < nblk)
+    const int blk = blockIdx.x * CPB + (int)threadIdx.x;
+    if (threadIdx.x < CPB && blk < nblk)
         blkcnt[b * nblk + blk] = sh[threadIdx.x][0] + sh[threadIdx.x][1] + sh[threadIdx.x][2] + sh[threadIdx.x][3];
 }
 
@@ -3350,8 +3356,12 @@ template <int KIND, bool EVD>
 struct CompactStage {
     static int run(const CompactArgs *a) {
         dim3 grid(a->nblk, a->b);
-        k_fg_count<KIND, EVD><<<dim3((a->nblk + kFgCPB - 1) / kFgCPB, a->b), 256, 0, a->s>>>(a->m, a->H, a->W, a->ws.blkcnt, a->ws.fgbits, a->nblk, a->ws.counts,
-                                                      a->ws.zero_words);
+        if ((int64_t)a->nblk * a->b > kFgWideAbove)
+            k_fg_count<KIND, EVD, kFgWideCPB><<<dim3((a->nblk + kFgWideCPB - 1) / kFgWideCPB, a->b), 256, 0, a->s>>>(
+                a->m, a->H, a->W, a->ws.blkcnt, a->ws.fgbits, a->nblk, a->ws.counts, a->ws.zero_words);
+        else
+            k_fg_count<KIND, EVD, 1><<<dim3(a->nblk, a->b), 256, 0, a->s>>>(a->m, a->H, a->W, a->ws.blkcnt, a->ws.fgbits,
+                                                                          a->nblk, a->ws.counts, a->ws.zero_words);
         if (a->vx.kind == PV_VERTEX_F32)
             k_compact<KIND, EVD, PV_VERTEX_F32><<<grid, 256, 0, a->s>>>(a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.fgbits, a->ws.dsagg,
                                                      a->nblk, a->min_num, a->max_num, a->seed, a->keep, a->ws.tn,
@@ -3476,7 +3486,7 @@ const char *pv_build_config(void) {
            PVV_STR(PVV_VM_RW3_1) "/" PVV_STR(PVV_VM_RW3_2) ")"
            " hypgen=" PVV_STR(PVV_HYPGEN)
            " refine=" PVV_STR(PVV_REFINE_NJ) "x" PVV_STR(PVV_REFINE_T)
-           " fg_cpb=" PVV_STR(PVV_FG_CPB) " compact_skip=" PVV_STR(PVV_COMPACT_SKIP)
+           " fg_cpb=1/" PVV_STR(8) " compact_skip=" PVV_STR(PVV_COMPACT_SKIP)
            " bytes=k_vote_bytes(rows=" PVV_STR(PVV_BYTE_HB) ",xcd=" PVV_STR(PVV_BYTES_XCD) ",bal=" PVV_STR(PVV_BYTES_BAL) ")"
 #ifdef PVV_TRACE
            " TRACE"

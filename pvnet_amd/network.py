@@ -426,6 +426,7 @@ def clear_conv_workspaces() -> None:
         _CAPTURE_WS.clear()
 
 CONV_SPLIT = True          # the split-K last round (A/B hook for tools/backbone_ab2.py; no environment switch)
+TAIL_SPLIT = True          # seg / ver as two dense maps from the fused tail (A/B hook for tools/e2e_vote_probe.py)
 
 
 def _conv_workspace(x: torch.Tensor, pixels: int, cout: int, ksteps: int):
@@ -602,11 +603,15 @@ def decoder_tail_weights(c0: nn.Conv2d, c1: nn.Conv2d, cin: int = 35):
             c1.bias.detach().float().contiguous())
 
 
-def decoder_tail(fm: torch.Tensor, img: torch.Tensor, weights, slope: float = 0.1) -> torch.Tensor:
+def decoder_tail(fm: torch.Tensor, img: torch.Tensor, weights, slope: float = 0.1, split: bool = False):
     """up2storaw + torch.cat([fm, x], 1) + convraw (MR:75-79) in one fp16
     matrix-core pass (``pv_decoder_tail_f16``): fm [n, 32, h, w] and img
     [n, 3, 2h, 2w] channels_last float16 CUDA; ``weights`` from
-    :func:`decoder_tail_weights`.  Returns [n, cout, 2h, 2w] channels_last."""
+    :func:`decoder_tail_weights`.  Returns [n, cout, 2h, 2w] channels_last;
+    with ``split`` (``pv_decoder_tail_split_f16``) the pair (seg [n, 2, 2h,
+    2w], ver [n, cout - 2, 2h, 2w]) as MR:79 slices them, each its own dense
+    channels_last map -- the voting layer's argmax then reads 4 bytes per
+    pixel, not the cache lines of the whole cout-channel record."""
     n, c, h, w = fm.shape
     cl = torch.channels_last
     if fm.dtype != torch.float16 or img.dtype != torch.float16 or not fm.is_cuda:
@@ -617,6 +622,13 @@ def decoder_tail(fm: torch.Tensor, img: torch.Tensor, weights, slope: float = 0.
         raise RuntimeError("decoder_tail: channels_last maps required")
     w1, b1, w2, b2 = weights
     cout = b2.numel()
+    if split:
+        seg = torch.empty((n, 2, 2 * h, 2 * w), dtype=fm.dtype, device=fm.device, memory_format=cl)
+        ver = torch.empty((n, cout - 2, 2 * h, 2 * w), dtype=fm.dtype, device=fm.device, memory_format=cl)
+        _dev_call("pv_decoder_tail_split_f16", None, fm, fm.data_ptr(), img.data_ptr(), w1.data_ptr(),
+                  b1.data_ptr(), w2.data_ptr(), b2.data_ptr(), seg.data_ptr(), ver.data_ptr(), n, h, w, cout,
+                  float(slope))
+        return seg, ver
     out = torch.empty((n, cout, 2 * h, 2 * w), dtype=fm.dtype, device=fm.device, memory_format=cl)
     _dev_call("pv_decoder_tail_f16", None, fm, fm.data_ptr(), img.data_ptr(), w1.data_ptr(), b1.data_ptr(),
               w2.data_ptr(), b2.data_ptr(), out.data_ptr(), n, h, w, cout, float(slope))
@@ -812,6 +824,8 @@ class PVNetInference(nn.Module):
             if getattr(self, "_tail_key", None) != key:     # matrix-core layouts of convraw's weights, made once
                 self._tail_w = decoder_tail_weights(c0, c1, self.raw_in)
                 self._tail_key = key
+            if self.seg_dim == 2 and TAIL_SPLIT:   # seg and ver as two dense maps (pv_decoder_tail_split_f16)
+                return decoder_tail(fm, x, self._tail_w, slope, split=True)
             out = decoder_tail(fm, x, self._tail_w, slope)
             return out[:, :self.seg_dim], out[:, self.seg_dim:]
         fm = upsample2x_cat(fm, x, self.raw_pad)

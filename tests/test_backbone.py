@@ -472,6 +472,14 @@ def test_decoder_tail_matches_torch(cout, hw, device):
     assert float(d.max()) <= tol
     assert float(d.mean()) <= 2 ** -12 * sc
     _check_decoder_fp64(got, fm, img, c0, 0.1, f"decoder tail cout {cout}", head=(c1.weight, c1.bias))
+    # the split form (pv_decoder_tail_split_f16): seg and ver as two dense
+    # channels_last maps, bit-equal to the one-buffer form's channel slices
+    with torch.no_grad():
+        seg, ver = decoder_tail(fm, img, decoder_tail_weights(c0, c1), 0.1, split=True)
+    torch.cuda.synchronize()
+    assert seg.shape == (n, 2, 2 * h, 2 * w) and ver.shape == (n, cout - 2, 2 * h, 2 * w)
+    assert seg.is_contiguous(memory_format=cl) and ver.is_contiguous(memory_format=cl)
+    assert torch.equal(seg, got[:, :2]) and torch.equal(ver, got[:, 2:])
 
 
 @pytest.mark.gpu

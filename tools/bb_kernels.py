@@ -29,6 +29,9 @@ import torch  # noqa: E402
 sys.path.insert(0, ".")
 from pvnet_amd.network import PVNet, PVNetInference  # noqa: E402
 
+import os  # noqa: E402
+import pvnet_amd.network as N  # noqa: E402
+N.TAIL_SPLIT = os.environ.get("TAIL_SPLIT", "1") != "0"
 torch.backends.cudnn.benchmark = True
 torch.manual_seed(0)
 dev = torch.device("cuda")
