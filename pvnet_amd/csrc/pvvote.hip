@@ -232,6 +232,7 @@ struct Workspace {
     int32_t *tn;        // [b] compacted pixels (0 = image skipped)
     int32_t *fgtot;     // [b] foreground before downsampling
     int32_t *blkcnt;    // [b][nblk]
+    int32_t *grpcnt;    // [b][ceil(nblk / kFgWideCPB)]: the wide k_fg_count blocks' sums (large grids only)
     uint64_t *fgbits;   // [b][nblk][4] foreground ballot of each wave of a k_fg_count block
     float4 *pex;        // [b][vn][P]   exact pixel data (cx, cy, nx, ny): reference operands
     float2 *hyp;        // [b][nh][vn]  (reference layout)
@@ -256,6 +257,7 @@ Workspace carve(void *base, int b, int H, int W, int vn, int nh) {
     w.tn = (int32_t *)take(4 * b);
     w.fgtot = (int32_t *)take(4 * b);
     w.blkcnt = (int32_t *)take(4 * b * nblk);
+    w.grpcnt = (int32_t *)take(4 * b * ((nblk + 7) / 8));
     w.fgbits = (uint64_t *)take(8 * 4 * b * nblk);
     w.pex = (float4 *)take(16 * b * vn * P);
     w.hyp = (float2 *)take(8 * (int64_t)b * nh * vn);
@@ -352,7 +354,7 @@ constexpr int kFgWideCPB = 8;
 constexpr int64_t kFgWideAbove = PVV_FG_WIDE_ABOVE;   // blocks of one chunk above which the wide form runs
 template <int KIND, bool EVD, int CPB>
 __global__ __launch_bounds__(256) void k_fg_count(MaskView m, int H, int W, int32_t *blkcnt, uint64_t *fgbits,
-                                                  int nblk, int32_t *zero, int64_t zero_words) {
+                                                  int32_t *grpcnt, int nblk, int32_t *zero, int64_t zero_words) {
     static_assert(kCompactChunk == 256, "one pixel per thread");
     const int b = blockIdx.y, wid = threadIdx.x / 64;
     const int64_t P = (int64_t)H * W;
@@ -385,6 +387,13 @@ __global__ __launch_bounds__(256) void k_fg_count(MaskView m, int H, int W, int3
     const int blk = blockIdx.x * CPB + (int)threadIdx.x;
     if (threadIdx.x < CPB && blk < nblk)
         blkcnt[b * nblk + blk] = sh[threadIdx.x][0] + sh[threadIdx.x][1] + sh[threadIdx.x][2] + sh[threadIdx.x][3];
+    if (CPB > 1 && threadIdx.x == 0) {   // the block's sum: k_compact's image totals read these
+        int g = 0;
+#pragma unroll
+        for (int k = 0; k < CPB; ++k)
+            if (blockIdx.x * CPB + k < nblk) g += sh[k][0] + sh[k][1] + sh[k][2] + sh[k][3];
+        grpcnt[b * gridDim.x + blockIdx.x] = g;
+    }
 }
 
 // foreground total of image b from the per-block counts (every block of K1b/K2 does this)
@@ -430,17 +439,17 @@ constexpr int kCompactKp = 12;   // keypoints whose vertex loads a compaction th
 constexpr uint64_t kLookbackSpin = 20000;   // s_memrealtime ticks (100 MHz): 200 us
 __device__ int g_lb_self;   // debug (pv_debug_lookback_self): every look-back count worked out by the waiter
 
-template <int KIND, bool EVD, int VK>
-__global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int H, int W, int vn,
-                                                 const int32_t *blkcnt, const uint64_t *fgbits, int32_t *dsagg,
-                                                 int nblk, int min_num, int max_num, uint64_t seed,
-                                                 const uint8_t *keep, int32_t *tn, int32_t *fgtot, float4 *pex) {
+// one chunk (256 pixels) of image b: the whole of a k_compact block
+// (block-uniform early returns; sh holds 8 ints, wcnt 4, pos 256 with TASKS)
+template <int KIND, bool EVD, int VK, bool TASKS>
+__device__ __forceinline__ void compact_chunk(const VertexView &vx, int H, int W, int vn, const int32_t *blkcnt,
+                                              const int32_t *grpcnt, const uint64_t *fgbits, int32_t *dsagg,
+                                              int nblk, int min_num, int max_num, uint64_t seed, const uint8_t *keep,
+                                              int32_t *tn, int32_t *fgtot, float4 *pex, const int b, const int blk,
+                                              int *sh, int *wcnt, uint16_t *pos) {
     static_assert(kCompactChunk == 256, "one pixel per thread");
-    const int b = blockIdx.y, blk = blockIdx.x;
     const int64_t P = (int64_t)H * W;
     const int wid = threadIdx.x / 64, lane = lane_id();
-    __shared__ int sh[8];
-    __shared__ int wcnt[4];
     cstamp(blk, 0);
 #if PVV_COMPACT_SKIP
     // a block without foreground has nothing to store; only blocks 0 and
@@ -452,7 +461,22 @@ __global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int 
     // one round trip: this wave's foreground ballot (k_fg_count) beside the
     // image's per-block counts (the total and this block's row-major offset)
     const uint64_t fw = fgbits[((int64_t)b * nblk + blk) * 4 + wid];
-    int2 tot = image_totals(blkcnt + b * nblk, nblk, blk, sh);
+    int2 tot;
+    if constexpr (TASKS) {
+        // the image's total and this chunk's prefix from the wide k_fg_count
+        // blocks' sums (8 chunks each) and the chunks before it in its group
+        const int ng = (nblk + 7) / 8, g0 = blk / 8;
+        int all = 0, pre = 0;
+        for (int j = threadIdx.x; j < ng; j += 256) {
+            const int v = grpcnt[b * ng + j];
+            all += v;
+            pre += j < g0 ? v : 0;
+        }
+        if (threadIdx.x < 8 && g0 * 8 + (int)threadIdx.x < blk) pre += blkcnt[b * nblk + g0 * 8 + threadIdx.x];
+        tot = block_sum2(all, pre, sh);
+    } else {
+        tot = image_totals(blkcnt + b * nblk, nblk, blk, sh);
+    }
     cstamp(blk, 1);
     const int fgb = tot.x;
     if (fgb < min_num) {
@@ -499,11 +523,14 @@ __global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int 
             }
         }
     };
-    load_group(0);
+    if constexpr (!TASKS) load_group(0);
     __syncthreads();
     const int nsel = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
     int off = below;
     for (int q = 0; q < wid; ++q) off += wcnt[q];
+    if constexpr (TASKS) {
+        if (f) pos[off] = (uint16_t)threadIdx.x;   // the block's selected pixels in rank order
+    }
     if (ds) {
         // Downsampled offsets by look-back: publish this block's kept count
         // (+1, so 0 = not yet; k_fg_count zeroed the array), then add up the
@@ -551,6 +578,32 @@ __global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int 
     // the selected pixel's records at t = base + its rank: consecutive
     // selected pixels write consecutive records of each keypoint
     float4 *eb = pex + (int64_t)b * vn * P;
+    if constexpr (TASKS) {
+        // one (selected pixel, keypoint) record per thread and pass, keypoint
+        // major: the block's nsel x vn records spread over all its lanes (with
+        // a sparse mask a lane-per-pixel store pass runs ~8 % of its lanes)
+        __syncthreads();   // pos written
+        const int n = nsel * vn;
+        const int s4 = uniform((int)(vx.s[4] * ES));
+        for (int i = (int)threadIdx.x; i < n; i += 256) {
+            const int v = (int)((uint32_t)i / (uint32_t)nsel), k = i - v * nsel;
+            const uint32_t pp = (uint32_t)blk * kCompactChunk + pos[k];
+            const int rr = (int)(pp / (uint32_t)W), cc = (int)(pp - (uint32_t)rr * W);
+            const int vo = (int)((rr * vx.s[1] + cc * vx.s[2] + v * vx.s[3]) * ES);
+            float x, y;
+            if constexpr (VK == PV_VERTEX_F32) {
+                x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vr, vo, 0, 0));
+                y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vr, vo, s4, 0));
+            } else {
+                x = __half2float(__ushort_as_half(__builtin_amdgcn_raw_buffer_load_b16(vr, vo, 0, 0)));
+                y = __half2float(__ushort_as_half(__builtin_amdgcn_raw_buffer_load_b16(vr, vo, s4, 0)));
+            }
+            const int64_t t = base + k;   // (bounded as below)
+            if (t < P) eb[(int64_t)v * P + t] = make_float4((float)cc, (float)rr, x, y);
+        }
+        cstamp(blk, 3);
+        return;
+    }
     const int64_t t = base + off;
     // t < fg <= P whenever the counts are this call's own; the bound keeps a
     // workspace shared by two calls in flight (a caller error) from writing
@@ -570,6 +623,22 @@ __global__ __launch_bounds__(256) void k_compact(MaskView m, VertexView vx, int 
         }
     }
     cstamp(blk, 3);
+}
+
+// TASKS (grids above kFgWideAbove blocks, i.e. batches): the records are
+// written by (pixel, keypoint) tasks spread over the block instead of by the
+// pixel's own lane (configs[2]'s 32 network frames, ~8 % foreground: 69 us)
+template <int KIND, bool EVD, int VK, bool TASKS>
+__global__ __launch_bounds__(256) void k_compact(MaskView, VertexView vx, int H, int W, int vn,
+                                                 const int32_t *blkcnt, const int32_t *grpcnt,
+                                                 const uint64_t *fgbits, int32_t *dsagg,
+                                                 int nblk, int min_num, int max_num, uint64_t seed,
+                                                 const uint8_t *keep, int32_t *tn, int32_t *fgtot, float4 *pex) {
+    __shared__ int sh[8];
+    __shared__ int wcnt[4];
+    __shared__ uint16_t pos[TASKS ? kCompactChunk : 1];
+    compact_chunk<KIND, EVD, VK, TASKS>(vx, H, W, vn, blkcnt, grpcnt, fgbits, dsagg, nblk, min_num, max_num, seed, keep, tn,
+                                        fgtot, pex, (int)blockIdx.y, (int)blockIdx.x, sh, wcnt, pos);
 }
 
 // ==========================================================================
@@ -3356,18 +3425,31 @@ template <int KIND, bool EVD>
 struct CompactStage {
     static int run(const CompactArgs *a) {
         dim3 grid(a->nblk, a->b);
+        static_assert(kFgWideCPB == 8, "grpcnt: groups of 8 chunks");
         if ((int64_t)a->nblk * a->b > kFgWideAbove)
             k_fg_count<KIND, EVD, kFgWideCPB><<<dim3((a->nblk + kFgWideCPB - 1) / kFgWideCPB, a->b), 256, 0, a->s>>>(
-                a->m, a->H, a->W, a->ws.blkcnt, a->ws.fgbits, a->nblk, a->ws.counts, a->ws.zero_words);
+                a->m, a->H, a->W, a->ws.blkcnt, a->ws.fgbits, a->ws.grpcnt, a->nblk, a->ws.counts, a->ws.zero_words);
         else
             k_fg_count<KIND, EVD, 1><<<dim3(a->nblk, a->b), 256, 0, a->s>>>(a->m, a->H, a->W, a->ws.blkcnt, a->ws.fgbits,
-                                                                          a->nblk, a->ws.counts, a->ws.zero_words);
+                                                                          nullptr, a->nblk, a->ws.counts,
+                                                                          a->ws.zero_words);
+        if ((int64_t)a->nblk * a->b > kFgWideAbove) {
+            if (a->vx.kind == PV_VERTEX_F32)
+                k_compact<KIND, EVD, PV_VERTEX_F32, true><<<grid, 256, 0, a->s>>>(
+                    a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.grpcnt, a->ws.fgbits, a->ws.dsagg, a->nblk, a->min_num,
+                    a->max_num, a->seed, a->keep, a->ws.tn, a->ws.fgtot, a->ws.pex);
+            else
+                k_compact<KIND, EVD, PV_VERTEX_F16, true><<<grid, 256, 0, a->s>>>(
+                    a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.grpcnt, a->ws.fgbits, a->ws.dsagg, a->nblk, a->min_num,
+                    a->max_num, a->seed, a->keep, a->ws.tn, a->ws.fgtot, a->ws.pex);
+            return last();
+        }
         if (a->vx.kind == PV_VERTEX_F32)
-            k_compact<KIND, EVD, PV_VERTEX_F32><<<grid, 256, 0, a->s>>>(a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.fgbits, a->ws.dsagg,
+            k_compact<KIND, EVD, PV_VERTEX_F32, false><<<grid, 256, 0, a->s>>>(a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.grpcnt, a->ws.fgbits, a->ws.dsagg,
                                                      a->nblk, a->min_num, a->max_num, a->seed, a->keep, a->ws.tn,
                                                      a->ws.fgtot, a->ws.pex);
         else
-            k_compact<KIND, EVD, PV_VERTEX_F16><<<grid, 256, 0, a->s>>>(a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.fgbits, a->ws.dsagg,
+            k_compact<KIND, EVD, PV_VERTEX_F16, false><<<grid, 256, 0, a->s>>>(a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.grpcnt, a->ws.fgbits, a->ws.dsagg,
                                                      a->nblk, a->min_num, a->max_num, a->seed, a->keep, a->ws.tn,
                                                      a->ws.fgtot, a->ws.pex);
         return last();

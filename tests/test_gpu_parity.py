@@ -457,6 +457,47 @@ def test_v3_batch_matches_single(device, rvg):
         np.testing.assert_allclose(kb[i], fb["keypoints"][i], atol=5.0)   # noisy field vs generator truth
 
 
+def test_v3_batch_wide_compaction(device, rvg):
+    """A batch large enough for the multi-chunk compaction (k_compact_wide:
+    more than 4,096 one-chunk blocks) -- five full frames, one of them below
+    min_num and one empty -- with and without downsampling (an injected
+    keep-mask at max_num 20,000; the chunks then go one by one through the
+    look-back).  Every image equals its own single call (the one-chunk
+    kernels) bit for bit, and the oracle's keypoints."""
+    from pvnet_amd import synth
+    b, hn = 5, 128
+    fb = synth.synthetic_batch(b, seed=300)
+    mask = np.argmax(fb["seg"], 1).astype(np.int64)
+    mask[3] = 0
+    mask[3, 100:105, 200:210] = 1          # 50 pixels: below min_num
+    mask[4] = 0                            # empty
+    vertex = np.ascontiguousarray(fb["vertex"].transpose(0, 2, 3, 1).reshape(b, 480, 640, 9, 2))
+    rng = np.random.default_rng(31)
+    keep = (rng.random((b, 480, 640)) < 0.6).astype(np.uint8)
+    for max_num, kp_keep in ((30000, None), (20000, keep)):
+        tn = [int(((mask[i] != 0) & (kp_keep[i] != 0 if kp_keep is not None else True)).sum()) for i in range(b)]
+        fg = [int((mask[i] != 0).sum()) for i in range(b)]
+        n_idx = [t if f > max_num else f for t, f in zip(tn, fg)]
+        idxs = np.stack([rng.integers(0, max(n, 1), (hn, 9, 2)) for n in n_idx]).astype(np.int32)
+        diag = {}
+        kb = rvg.ransac_voting_layer_v3(cu(mask, device), cu(vertex, device), hn, max_num=max_num, _idxs=idxs,
+                                        _keep=kp_keep, _diag=diag).cpu().numpy()
+        for i in range(b):
+            d1 = {}
+            k1 = rvg.ransac_voting_layer_v3(cu(mask[i:i + 1], device), cu(vertex[i:i + 1], device), hn,
+                                            max_num=max_num, _idxs=idxs[i:i + 1],
+                                            _keep=None if kp_keep is None else kp_keep[i:i + 1],
+                                            _diag=d1).cpu().numpy()
+            assert int(diag["tn"][i]) == int(d1["tn"][0]), (max_num, i)
+            np.testing.assert_array_equal(diag["counts"][i].cpu().numpy(), d1["counts"][0].cpu().numpy())
+            np.testing.assert_array_equal(kb[i], k1[0])
+            ko = O.ransac_voting_layer_v3(mask[i:i + 1], vertex[i:i + 1], hn, max_num=max_num, idxs=[idxs[i]],
+                                          keep=None if kp_keep is None else [kp_keep[i]])
+            np.testing.assert_allclose(kb[i], ko[0], atol=KP_TOL)
+        assert int(diag["tn"][3]) == 0 and int(diag["tn"][4]) == 0
+        assert int(diag["tn"][0]) == (n_idx[0] if max_num == 20000 else fg[0])
+
+
 # ---------------------------------------------------------------- EVD
 @pytest.mark.parametrize("case", ["cat_evdm", "synth_evdm"])
 def test_evd_with_mean(case, device, rvg):
