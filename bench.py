@@ -76,12 +76,17 @@ def new_stream(dev):
     return st
 
 
+_GRAPHS = []
+
+
 def new_graph():
-    """A hipGraph, dropped when its last user lets go of it (round 4 kept
-    every graph for the whole process after a many-graph probe died once; the
-    same churn -- tools/extra_kernel_probe.py, 12 bench-size graphs captured,
-    replayed and dropped in turn -- runs clean: DESIGN.md "Concurrent callers")."""
-    return torch.cuda.CUDAGraph()
+    """A hipGraph kept alive for the whole process (with the streams it was
+    captured on): round 5's host SIGSEGV in a variant build's bench run has
+    no surviving record, so no graph is destroyed while the
+    process runs."""
+    g = torch.cuda.CUDAGraph()
+    _GRAPHS.append(g)
+    return g
 
 
 def log(*a):
@@ -142,6 +147,107 @@ def visible_gpus():
     return n
 
 
+def _parse_cpulist(s):
+    out = set()
+    for part in s.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.update(range(int(a), int(b or a) + 1))
+    return out
+
+
+def _fmt_cpulist(cpus):
+    cpus, runs = sorted(cpus), []
+    for c in cpus:
+        if runs and c == runs[-1][1] + 1:
+            runs[-1][1] = c
+        else:
+            runs.append([c, c])
+    return ",".join(f"{a}-{b}" if a != b else str(a) for a, b in runs)
+
+
+def gpu_local_cpus():
+    """Per visible GPU (HIP's order), the CPUs local to it, from sysfs only
+    (no HIP call): KFD topology nodes with SIMDs in node order -> the PCI
+    device of each (domain, location_id = bus << 8 | dev << 3 | fn) ->
+    /sys/bus/pci/devices/<bdf>/local_cpulist.  Cut by *_VISIBLE_DEVICES
+    when that is a list of indices.  None if sysfs is unreadable."""
+    import glob
+    try:
+        nodes = []
+        for p in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+            with open(p) as f:
+                props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+            if int(props.get("simd_count", "0")) > 0:
+                nodes.append((int(p.split("/")[-2]), int(props.get("domain", "0")), int(props["location_id"])))
+        nodes.sort()
+        cpus = []
+        for _, dom, loc in nodes:
+            bdf = f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 31:02x}.{loc & 7}"
+            with open(f"/sys/bus/pci/devices/{bdf}/local_cpulist") as f:
+                cpus.append(_parse_cpulist(f.read()))
+    except (OSError, ValueError, KeyError):
+        return None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            try:
+                cpus = [cpus[int(x)] for x in v.split(",") if x.strip() != ""]
+            except (ValueError, IndexError):
+                return None
+    return cpus
+
+
+def rank_cpu_sets(nranks, allowed, local=None, share_device=False):
+    """Disjoint CPU sets for local ranks 0..nranks-1 (rank r drives GPU r,
+    or GPU 0 for every rank with --share-device): each GPU's local CPUs
+    within ``allowed`` (this process's affinity), split evenly between the
+    ranks on the same set of local CPUs.  Falls back to an even split of
+    ``allowed`` when the topology is unknown or the per-GPU sets overlap
+    without being equal.  Returns (sets, source) or (None, reason) when
+    there are fewer CPUs than ranks."""
+    allowed = set(allowed)
+    groups, source = None, "even-split"
+    if local is not None and (share_device or len(local) >= nranks):
+        per = [set(local[0 if share_device else r]) & allowed for r in range(nranks)]
+        keys = {frozenset(s) for s in per}
+        if all(per) and all(a == b or not (a & b) for a in keys for b in keys):
+            groups, source = {}, "gpu-local"
+            for r, s in enumerate(per):
+                groups.setdefault(frozenset(s), []).append(r)
+    if groups is None:
+        groups = {frozenset(allowed): list(range(nranks))}
+    out = [None] * nranks
+    for cpus, ranks in groups.items():
+        cl = sorted(cpus)
+        k = len(ranks)
+        if len(cl) < k:
+            return None, f"{len(cl)} cpus for {k} ranks"
+        for i, r in enumerate(ranks):
+            out[r] = set(cl[i * len(cl) // k:(i + 1) * len(cl) // k])
+    return out, source
+
+
+def pin_rank(args):
+    """Before the rank's first GPU call: pin this process to its disjoint
+    share of the CPUs near its GPU (rank_cpu_sets; one host thread submits
+    the rank's graph replays, DESIGN.md 8).  Only with more than one rank;
+    PVNET_NO_PIN=1 turns it off.  Returns (cpulist string, source)."""
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    cur = os.sched_getaffinity(0)
+    if ws <= 1 or os.environ.get("PVNET_NO_PIN") == "1":
+        return _fmt_cpulist(cur), "unpinned"
+    lw = int(os.environ.get("LOCAL_WORLD_SIZE", str(ws)))
+    lr = int(os.environ.get("LOCAL_RANK", "0"))
+    sets, source = rank_cpu_sets(lw, cur, None if args.dry_run else gpu_local_cpus(),
+                                 share_device=args.share_device)
+    if sets is None:
+        return _fmt_cpulist(cur), f"unpinned ({source})"
+    os.sched_setaffinity(0, sets[lr])
+    return _fmt_cpulist(sets[lr]), source
+
+
 def launch_ranks(args):
     """`bench.py --gpus N` (N > 1) outside torchrun: start the N ranks as child
     processes (the script again, RANK = LOCAL_RANK = r, WORLD_SIZE = N,
@@ -193,6 +299,15 @@ def launch_ranks(args):
         stop()
         raise
     return rc
+
+
+def gather_rank_cpus(args, ws):
+    """Every rank's CPU list (pin_rank), in rank order, for the line."""
+    if ws <= 1:
+        return [args.rank_cpus[0]]
+    allc = [None] * ws
+    dist.all_gather_object(allc, args.rank_cpus[0])
+    return allc
 
 
 def setup_dist(args):
@@ -413,7 +528,8 @@ def dry_run(args, ws, rank):
                 "vs_baseline": None, "dtype": "f32", "data": "none (dry run)", "dry_run": True,
                 "config": {"workload": "dry run: launcher + shard + gather only, no voting", "global_batch": M * ws,
                            "per_gpu_batch_per_step": M, "stream_images": n_images},
-                "stream_order_max_err_px": err, "stream_order_ok": err == 0.0}
+                "stream_order_max_err_px": err, "stream_order_ok": err == 0.0,
+                "rank_cpus": args.rank_cpus_all, "rank_cpus_source": args.rank_cpus[1]}
         assert line["n_gpus"] == args.gpus
         if not args.skip_cpu:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
@@ -428,7 +544,9 @@ def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         raise SystemExit(launch_ranks(args))
+    args.rank_cpus = pin_rank(args)      # before any GPU call
     ws, rank, dev = setup_dist(args)
+    args.rank_cpus_all = gather_rank_cpus(args, ws)
     if args.dry_run:
         return dry_run(args, ws, rank)
     from pvnet_amd import ransac_voting_gpu as rvg
@@ -1224,6 +1342,8 @@ def report(args, ws, res, final_err, dev):
         "stream_order_ok": res["order_err"] <= 5.0,
         "latency_ms_per_image": round(res["latency_ms"], 5),
         "host_ms_per_replay": round(res["host_ms_per_replay"], 4),
+        "rank_cpus": args.rank_cpus_all,
+        "rank_cpus_source": args.rank_cpus[1],
         "library": library_config(),
     }
     if res.get("batched") is not None:

@@ -257,7 +257,6 @@ __device__ __forceinline__ void halo_blend(const TailArgs &a, const _Float16 *pa
 #define PVT_WREG 12          // k-steps whose weights stay in registers (cout <= 32; 2 fewer above); the rest in LDS
 #endif
 
-#if PVT_V1
 // The head's output stores: 4 channels o0 .. o0 + 3 of one pixel (8 bytes).
 // Unsplit, [N][H][W][cout] at 2 * (cout pix + o0).  Split (pv_decoder_tail_split_f16),
 // channels 0-1 go to seg [N][H][W][2] and the rest to the vertex map [N][H][W][cout - 2]:
@@ -293,6 +292,7 @@ __device__ __forceinline__ void tail_store(const TailOut &t, int pix, int o0, h4
     }
 }
 
+#if PVT_V1
 template <int COUT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVT_WPE, PVT_WPE))) void k_decoder_tail(TailArgs a) {
     constexpr int MT = (COUT + 31) / 32;

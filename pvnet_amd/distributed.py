@@ -41,8 +41,13 @@ def gather_results(local: torch.Tensor, n_images: int, rank: int, world: int,
     """
     per = (n_images + world - 1) // world
     feat = tuple(local.shape[1:])
-    if world == 1 and not (dist.is_available() and dist.is_initialized()):
-        return local        # no process group: nothing to exchange (with one, the collective runs: a copy)
+    grouped = dist.is_available() and dist.is_initialized()
+    if grouped and dist.get_world_size(group) != world:
+        if world != 1:
+            raise ValueError(f"world {world} differs from the process group's size {dist.get_world_size(group)}")
+        grouped = False     # a local-only gather inside a multi-rank job
+    if world == 1 and not grouped:
+        return local        # nothing to exchange (in a one-rank group the collective runs: a copy)
     if local.shape[0] != len(range(rank, n_images, world)):
         raise ValueError(f"rank {rank} holds {local.shape[0]} results, its shard has {len(range(rank, n_images, world))}")
     # RCCL moves device tensors over xGMI; gloo (the CPU tests, or ranks that

@@ -63,7 +63,10 @@ class VotingWorkspace:
       call at a time: an eager call on a stream other than the one its
       previous call ran on raises ``RuntimeError`` if that call is still in
       flight (an event recorded after each call), so two threads handing one
-      workspace to their own streams get an error, not a race.  Inside a
+      workspace to their own streams get an error, not a race.  The check is
+      host-side: it cannot see a ``wait_stream`` that orders the two streams,
+      so a caller that orders them itself passes ``check_streams=False``.
+      Inside a
       graph capture there is no check (the call runs when the graph is
       replayed): a workspace captured into a graph belongs to that graph, and
       two graphs that may replay at the same time need one each.  Growing
@@ -80,10 +83,11 @@ class VotingWorkspace:
     that used it, so the caching allocator never hands it out while a kernel
     can still touch it.  Thread-safe (one lock per workspace)."""
 
-    def __init__(self, per_stream: bool = False):
+    def __init__(self, per_stream: bool = False, check_streams: bool = True):
         self._buf = {}
         self._streams = {}
         self._per_stream = per_stream
+        self._check = check_streams
         self._lock = threading.Lock()
         self._owner = {}       # explicit: key -> [stream handle of the last call, busy, event after it]
 
@@ -98,12 +102,13 @@ class VotingWorkspace:
             return torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
         key = self._key(device, stream)
         with self._lock:
+            own = None
             if not self._per_stream and not capturing:
                 own = self._owner.setdefault(key, [stream.cuda_stream, False, None])
-                if own[0] != stream.cuda_stream and (own[1] or (own[2] is not None and not own[2].query())):
+                if self._check and own[0] != stream.cuda_stream and \
+                        (own[1] or (own[2] is not None and not own[2].query())):
                     raise RuntimeError("VotingWorkspace is in use by a call in flight on another stream: give each "
                                        "stream (each launching thread) its own workspace")
-                own[0], own[1] = stream.cuda_stream, True
             buf = self._buf.get(key)
             if buf is None or buf.numel() < nbytes:
                 if capturing:
@@ -116,6 +121,9 @@ class VotingWorkspace:
                 self._buf[key] = buf
                 self._streams[key] = set()
             self._streams[key].add(stream)
+            if own is not None:
+                # busy only once the buffer is in hand: a failed allocation leaves the workspace free
+                own[0], own[1] = stream.cuda_stream, True
             return buf
 
     def done(self, device) -> None:

@@ -76,3 +76,51 @@ def test_launcher_two_ranks_on_the_device():
     assert line["config"]["stream_images"] == 2 * 2 * 16
     assert line["stream_config3"]["n_gpus"] == 2 and line["stream_config3"]["zeros_path_ok"]
     assert line["stream_config4"]["n_gpus"] == 2 and line["stream_config4"]["covariances_finite"]
+
+
+def _cpuset(s):
+    out = set()
+    for part in s.split(","):
+        a, _, b = part.partition("-")
+        out.update(range(int(a), int(b or a) + 1))
+    return out
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_launcher_ranks_pinned_disjoint(n):
+    """bench.pin_rank: every rank of `bench.py --gpus N` runs on its own CPUs
+    (set before its first GPU call), disjoint from the other ranks', reported
+    in the line as rank_cpus."""
+    p = _run("--gpus", str(n), "--skip-cpu")
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    sets = [_cpuset(s) for s in line["rank_cpus"]]
+    assert len(sets) == n and all(sets)
+    for i in range(n):
+        for j in range(i + 1, n):
+            assert not (sets[i] & sets[j]), line["rank_cpus"]
+    assert set().union(*sets) <= os.sched_getaffinity(0)
+    assert line["rank_cpus_source"] == "even-split"      # no KFD topology in this container
+
+
+def test_rank_cpu_sets_gpu_local():
+    """rank_cpu_sets on a modelled 8-GPU node: GPUs 0-3 local to CPUs 0-63,
+    GPUs 4-7 to 64-127, the process allowed every other CPU: each rank gets
+    its own slice of its GPU's local CPUs."""
+    import bench
+    local = [set(range(0, 64))] * 4 + [set(range(64, 128))] * 4
+    allowed = set(range(0, 128, 2))
+    sets, src = bench.rank_cpu_sets(8, allowed, local)
+    assert src == "gpu-local"
+    for r in range(8):
+        assert sets[r] and sets[r] <= local[r] & allowed and len(sets[r]) == 8
+        for q in range(r):
+            assert not (sets[r] & sets[q])
+    # overlapping but unequal local sets: an even split of the allowed CPUs
+    sets, src = bench.rank_cpu_sets(2, set(range(8)), [set(range(0, 6)), set(range(2, 8))])
+    assert src == "even-split" and sets == [set(range(4)), set(range(4, 8))]
+    # --share-device: every rank on GPU 0's local CPUs
+    sets, src = bench.rank_cpu_sets(2, set(range(16)), [set(range(8))], share_device=True)
+    assert src == "gpu-local" and sets == [set(range(4)), set(range(4, 8))]
+    # fewer CPUs than ranks: no pinning
+    assert bench.rank_cpu_sets(4, {0, 1}, None)[0] is None

@@ -285,3 +285,54 @@ def test_two_threads_split_conv_graphs_shared_capture_stream(device):
     for i in range(2):
         for o in got[i]:
             assert torch.equal(o, ref[i])
+
+
+_RELEASE_CHILD = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, %r)
+from pvnet_amd import streams, ransac_voting_gpu as rvg
+from tests import golden_io as G
+gs = G.load("synth_v3_512")
+_, _, fs = G.synth_inputs(gs)
+dev = torch.device("cuda:0")
+torch.cuda.set_device(dev)
+seg, ver = torch.from_numpy(fs["seg"]).to(dev), torch.from_numpy(fs["vertex"]).to(dev)
+idxs = torch.from_numpy(np.ascontiguousarray(gs["idxs"])).to(dev, torch.int32)
+res = []
+for r in range(3):
+    st = streams.new_stream(dev)
+    ws = rvg.VotingWorkspace()
+    out = torch.zeros((1, 9, 2), device=dev)
+    with torch.cuda.stream(st):
+        rvg.ransac_voting_layer_v3_from_network(seg, ver, 512, _idxs=idxs, _workspace=ws, out=out)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            rvg.ransac_voting_layer_v3_from_network(seg, ver, 512, _idxs=idxs, _workspace=ws, out=out)
+        out.zero_()
+        g.replay()
+    st.synchronize()
+    res.append(out.cpu().numpy().copy())
+    del g, ws
+    streams.release(st, destroy=(r != 1))
+assert streams.live_count() == 0
+assert all(np.array_equal(res[0], x) for x in res[1:]), "results differ across re-created streams"
+np.testing.assert_allclose(res[0], gs["keypoints"], atol=1e-2, rtol=0)
+print("release-cycle ok", flush=True)
+"""
+
+
+def test_streams_release_recreate_bit_equal_exit_zero():
+    """pvnet_amd.streams.release: a process creates a stream,
+    votes on it eagerly and through a graph captured on it, drops the graph
+    and workspace, releases the stream (destroyed twice, kept for reuse once)
+    and creates the next; all three rounds bit-equal and within the golden
+    tolerance, nothing left live, and the process exits 0 (round 5's exit
+    crash came from streams destroyed at interpreter exit)."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-X", "faulthandler", "-c", _RELEASE_CHILD % repo], cwd=repo,
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, f"exit {p.returncode}\n{p.stdout[-2000:]}\n{p.stderr[-4000:]}"
+    assert "release-cycle ok" in p.stdout
