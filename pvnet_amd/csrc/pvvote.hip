@@ -51,6 +51,11 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kCompactChunk = 256;           // pixels per compaction block (one per thread)
+constexpr int kFrontPx = 2048;               // pixels per k_front block
+constexpr int kFrontT = 512;                 // k_front block threads (8 waves, 4 pixels each)
+constexpr int kFrontNW = kFrontT / 64;
+constexpr int kFrontK = kFrontPx / kFrontT;
+constexpr int kFrontWords = kFrontPx / 64;   // wave ballots per k_front block
 constexpr int kVoteChunk = 256;              // pixels per LDS-staged sub-chunk of the vote waves
 // refine blocks per (image, keypoint); measured with the gathering hand-off
 // (tools/ab_libs.sh, two rounds, stream images/s and sequential latency):
@@ -224,6 +229,9 @@ __device__ __forceinline__ bool is_fg(const MaskView &m, int b, int r, int c) {
 // workspace
 // --------------------------------------------------------------------------
 struct Workspace {
+    uint64_t *fhdr;     // k_front's header at offset 0 of every workspace: [0] epoch (low 32 bits), [1] ticket
+    uint64_t *fflag;    // [2][b][nfb]   k_front's tagged count flags (all-gather; round 2: downsampled counts)
+    uint64_t *fbal;     // [b][nfb][32]  k_front's (kept) pixel ballots, published before the flags
     int32_t *counts;    // [b][vn][nh]   zeroed by k_fg_count
     uint4 *refslot;     // [b][vn][kRefineNJ][kRefineGran] zeroed by k_fg_count: k_refine_solve's tagged partials
     int32_t *dsagg;     // [b][nblk]     zeroed by k_fg_count: downsampled count + 1 per block (look-back)
@@ -247,6 +255,13 @@ Workspace carve(void *base, int b, int H, int W, int vn, int nh) {
     char *p = (char *)base;
     int64_t off = 0;
     auto take = [&](int64_t bytes) { char *q = p ? p + off : nullptr; off = align_up(off + bytes, 256); return q; };
+    // k_front's header and flags first: their place does not depend on the
+    // shape, so flags a call left are only ever read as flags (tagged by the
+    // header's epoch, which only grows) whatever shape the next call has
+    const int64_t nfb = (P + kFrontPx - 1) / kFrontPx;
+    w.fhdr = (uint64_t *)take(256);
+    w.fflag = (uint64_t *)take(16 * b * nfb);
+    w.fbal = (uint64_t *)take(8 * kFrontWords * b * nfb);
     const int64_t ncnt = align_up((int64_t)b * vn * nh, 4);            // refslot 16-B aligned
     const int64_t nslot = (int64_t)b * vn * kRefineNJ * kRefineGran;
     w.zero_words = ncnt + 4 * nslot + b * nblk + 2 * (int64_t)b * vn;
@@ -625,20 +640,493 @@ __device__ __forceinline__ void compact_chunk(const VertexView &vx, int H, int W
     cstamp(blk, 3);
 }
 
+// ==========================================================================
+// K3 inside K2 (round 6): the hypotheses (KU:11-49, RV:553-557) made by the
+// first `nhb` blocks of k_compact's grid, beside the compaction, instead of a
+// k_hyp_gen launch after it.  Everything they need is k_fg_count's (the
+// kernel before): the image's chunk counts give tn and a chunk prefix (LDS),
+// a pair index t finds its chunk by binary search and its pixel by a bit
+// select in that chunk's four wave ballots, and the pixel's direction is read
+// from the input view -- the same (col, row, nx, ny) k_compact stores as its
+// record, so the hypotheses are bit-identical to k_hyp_gen's.  Downsampled
+// images (fg > max_num) rank the kept pixels: kept counts from the
+// compaction blocks' look-back values (a count not seen within kLookbackSpin
+// is worked out from the ballots and keep decisions), kept bits by the same
+// keep decision.  One dependent trip more than a compaction block (the
+// ballots), one kernel fewer in the call's chain: a k_hyp_gen launch costs
+// the batch-1 stream ~9 % (profiles/r06/ablation.txt).
+// ==========================================================================
+constexpr int kHypMaxChunks = 1536;   // chunks per image the fused hypotheses handle (LDS prefix); more: k_hyp_gen
+struct HypGen {
+    int nhb;                    // hypothesis blocks per image (0: none, k_hyp_gen runs)
+    int nh, vn, min_num, max_num;
+    uint64_t seed;              // the hypotheses' counter RNG (VoteArgs::seed)
+    uint64_t kseed;             // the downsampling keep decisions' (k_compact's seed)
+    const int32_t *idxs;        // [b][nh][vn][2] pixel pairs, or nullptr (counter RNG)
+    const uint8_t *keep;
+    float2 *hyp_out;            // [b][nh][vn]
+    float2 *hypv_out;           // [b][vn][nh]
+    float *diag_hyp;            // [b][nh][vn][2] or nullptr
+};
+
+template <int VK>
+__device__ __forceinline__ void read_dir(const __amdgpu_buffer_rsrc_t &vr, int voff, int s4, float &x, float &y) {
+    if constexpr (VK == PV_VERTEX_F32) {
+        x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vr, voff, 0, 0));
+        y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vr, voff, s4, 0));
+    } else {
+        x = __half2float(__ushort_as_half(__builtin_amdgcn_raw_buffer_load_b16(vr, voff, 0, 0)));
+        y = __half2float(__ushort_as_half(__builtin_amdgcn_raw_buffer_load_b16(vr, voff, s4, 0)));
+    }
+}
+
+// the q-th set bit (0-based) of the 256-bit mask w[0..3]; q < popcount
+__device__ __forceinline__ int select_bit(const uint64_t (&w)[4], int q) {
+    int base = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int c = __popcll(w[k]);
+        if (q < c) {
+            uint64_t x = w[k];
+            uint32_t lo = (uint32_t)x;
+            int off = 0;
+            if (q >= __popc(lo)) { q -= __popc(lo); lo = (uint32_t)(x >> 32); off = 32; }
+            // binary descent on the 32-bit half
+            int pos = 0;
+#pragma unroll
+            for (int sh = 16; sh >= 1; sh >>= 1) {
+                const int c2 = __popc(lo & ((1u << sh) - 1u));
+                if (q >= c2) { q -= c2; lo >>= sh; pos += sh; }
+            }
+            return base + off + pos;
+        }
+        q -= c;
+        base += 64;
+    }
+    return 255;
+}
+
+template <int KIND, bool EVD, int VK>
+__device__ void compact_hyp(const VertexView &vx, int H, int W, int nblk, const int32_t *blkcnt,
+                            const uint64_t *fgbits, const int32_t *dsagg, int32_t *pre, int *sh, const HypGen &g,
+                            int b, int hb) {
+    const int64_t P = (int64_t)H * W;
+    const int per = (nblk + 255) / 256;            // consecutive chunks per thread (<= 6)
+    // ---- the image's chunk counts and their exclusive prefix (one trip)
+    int c[6];
+    const int j0 = (int)threadIdx.x * per;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) c[k] = k < per && j0 + k < nblk ? blkcnt[b * nblk + j0 + k] : 0;
+    auto scan = [&](int (&v)[6]) -> int {        // block exclusive scan into pre[], returns the total
+        int run = 0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) run += v[k];
+        // inclusive wave scan of run (row shifts + row broadcasts)
+        int x = run;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (lane_id() >= o) x += y;
+        }
+        __syncthreads();
+        if (lane_id() == 63) sh[threadIdx.x / 64] = x;
+        __syncthreads();
+        int wpre = 0;
+        for (int w = 0; w < (int)threadIdx.x / 64; ++w) wpre += sh[w];
+        const int total = sh[0] + sh[1] + sh[2] + sh[3];
+        int e = wpre + x - run;
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            if (k < per && j0 + k < nblk) { pre[j0 + k] = e; e += v[k]; }
+        if (threadIdx.x == 0) pre[nblk] = total;
+        __syncthreads();
+        return total;
+    };
+    const int fgb = scan(c);
+    if (fgb < g.min_num) return;                   // tn = 0: no hypotheses (as k_hyp_gen)
+    const bool ds = fgb > g.max_num;
+    const float pk = (float)g.max_num / (float)fgb;
+    auto kept = [&](int64_t p) -> bool {
+        return g.keep ? g.keep[b * P + p] != 0 : rand_unit(g.kseed, (uint64_t)b * P + p) < pk;
+    };
+    int n = fgb;
+    if (ds) {
+        // kept counts from the compaction blocks' look-back values (count + 1)
+        const uint64_t t_dead = __builtin_amdgcn_s_memrealtime() + kLookbackSpin;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const int j = j0 + k;
+            if (!(k < per && j < nblk) || c[k] == 0) { c[k] = 0; continue; }
+            int v = g_lb_self ? 0 : ld_agent(&dsagg[b * nblk + j]);
+            while (v == 0 && !g_lb_self && __builtin_amdgcn_s_memrealtime() < t_dead) {
+                __builtin_amdgcn_s_sleep(1);
+                v = ld_agent(&dsagg[b * nblk + j]);
+            }
+            if (v == 0) {                          // worked out from the ballots and keep decisions
+                for (int q = 0; q < 4; ++q) {
+                    uint64_t w = fgbits[((int64_t)b * nblk + j) * 4 + q];
+                    while (w) {
+                        v += kept((int64_t)j * kCompactChunk + q * 64 + __builtin_ctzll(w));
+                        w &= w - 1;
+                    }
+                }
+                ++v;
+            }
+            c[k] = v - 1;
+        }
+        n = scan(c);
+    }
+    n = min(n, (int)P);
+    if (n <= 0) return;
+    // ---- this thread's hypothesis: item i = (h, v) of image b
+    const int i = hb * 256 + (int)threadIdx.x;
+    if (i >= g.nh * g.vn) return;
+    const int h = i / g.vn, v = i - h * g.vn;
+    const int64_t gid = ((int64_t)b * g.nh + h) * g.vn + v;
+    int t[2];
+    if (g.idxs) {
+        t[0] = min(max(g.idxs[gid * 2], 0), n - 1);
+        t[1] = min(max(g.idxs[gid * 2 + 1], 0), n - 1);
+    } else {
+        const uint64_t key = (uint64_t)gid;
+        t[0] = rand_index(g.seed, key * 2, n);
+        t[1] = rand_index(g.seed, key * 2 + 1, n);
+    }
+    int jj[2], rr[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {                  // the last chunk with pre <= t (never an empty one)
+        int lo = 0, hi = nblk - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (pre[mid] <= t[e]) lo = mid; else hi = mid - 1;
+        }
+        jj[e] = lo;
+        rr[e] = t[e] - pre[lo];
+    }
+    uint64_t w0[4], w1[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        w0[q] = fgbits[((int64_t)b * nblk + jj[0]) * 4 + q];
+        w1[q] = fgbits[((int64_t)b * nblk + jj[1]) * 4 + q];
+    }
+    if (ds) {                                      // keep only the kept pixels' bits
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint64_t m0 = 0, m1 = 0, x0 = w0[q], x1 = w1[q];
+            while (x0) { const int z = __builtin_ctzll(x0); x0 &= x0 - 1;
+                         if (kept((int64_t)jj[0] * kCompactChunk + q * 64 + z)) m0 |= 1ull << z; }
+            while (x1) { const int z = __builtin_ctzll(x1); x1 &= x1 - 1;
+                         if (kept((int64_t)jj[1] * kCompactChunk + q * 64 + z)) m1 |= 1ull << z; }
+            w0[q] = m0; w1[q] = m1;
+        }
+    }
+    constexpr int ES = VK == PV_VERTEX_F32 ? 4 : 2;
+    const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)((const char *)vx.p + (int64_t)b * vx.s[0] * ES), (short)0, vx.extent, 0x00020000);
+    const int s4 = (int)(vx.s[4] * ES);
+    float cx[2], cy[2], nx[2], ny[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const int q = select_bit(e == 0 ? w0 : w1, rr[e]);
+        const uint32_t p = (uint32_t)jj[e] * kCompactChunk + (uint32_t)q;
+        const int r = (int)(p / (uint32_t)W), col = (int)(p - (uint32_t)r * W);
+        cx[e] = (float)col;
+        cy[e] = (float)r;
+        read_dir<VK>(vr, (int)((r * vx.s[1] + col * vx.s[2] + v * vx.s[3]) * ES), s4, nx[e], ny[e]);
+    }
+    float x = 0.f, y = 0.f, ox, oy;
+    if (exact_intersect(nx[0], ny[0], cx[0], cy[0], nx[1], ny[1], cx[1], cy[1], &ox, &oy)) { x = ox; y = oy; }
+    g.hyp_out[gid] = make_float2(x, y);
+    if (g.diag_hyp) { g.diag_hyp[gid * 2] = x; g.diag_hyp[gid * 2 + 1] = y; }
+    g.hypv_out[((int64_t)b * g.vn + v) * g.nh + h] = make_float2(x, y);
+}
+
 // TASKS (grids above kFgWideAbove blocks, i.e. batches): the records are
 // written by (pixel, keypoint) tasks spread over the block instead of by the
-// pixel's own lane (configs[2]'s 32 network frames, ~8 % foreground: 69 us)
+// pixel's own lane (configs[2]'s 32 network frames, ~8 % foreground: 69 us).
+// With g.nhb > 0 the grid's first g.nhb blocks per image make the hypotheses.
 template <int KIND, bool EVD, int VK, bool TASKS>
 __global__ __launch_bounds__(256) void k_compact(MaskView, VertexView vx, int H, int W, int vn,
                                                  const int32_t *blkcnt, const int32_t *grpcnt,
                                                  const uint64_t *fgbits, int32_t *dsagg,
                                                  int nblk, int min_num, int max_num, uint64_t seed,
-                                                 const uint8_t *keep, int32_t *tn, int32_t *fgtot, float4 *pex) {
+                                                 const uint8_t *keep, int32_t *tn, int32_t *fgtot, float4 *pex,
+                                                 HypGen g) {
     __shared__ int sh[8];
     __shared__ int wcnt[4];
     __shared__ uint16_t pos[TASKS ? kCompactChunk : 1];
+    __shared__ int32_t pre[kHypMaxChunks + 1];
+    if ((int)blockIdx.x < g.nhb) {
+        compact_hyp<KIND, EVD, VK>(vx, H, W, nblk, blkcnt, fgbits, dsagg, pre, sh, g, (int)blockIdx.y, (int)blockIdx.x);
+        return;
+    }
     compact_chunk<KIND, EVD, VK, TASKS>(vx, H, W, vn, blkcnt, grpcnt, fgbits, dsagg, nblk, min_num, max_num, seed, keep, tn,
-                                        fgtot, pex, (int)blockIdx.y, (int)blockIdx.x, sh, wcnt, pos);
+                                        fgtot, pex, (int)blockIdx.y, (int)blockIdx.x - g.nhb, sh, wcnt, pos);
+}
+
+// ==========================================================================
+// K1 + K2 in one launch (round 6): k_front, the compaction of a small batch
+// (RV:533-552) by fat blocks of kFrontPx pixels, 8 per thread.
+//  1. each block counts its foreground (mask, or seg_pred's argmax), stores
+//     its 32 wave ballots and publishes its count as a tagged flag
+//     {epoch + 1, count} (agent-scope stores, ballots first);
+//  2. each block reads every flag of its image -- an all-gather, not a serial
+//     look-back: one image's blocks run side by side -- and so knows the
+//     image's total and its own row-major offset;
+//  3. fg > max_num: keep decisions (RV:543-546), kept ballots, a second
+//     tagged round of the same form;
+//  4. the block's kept pixels' records, (pixel, keypoint) tasks spread over
+//     its threads (a block of the object's interior holds ~600 of them).
+// No state has to be zeroed between calls: the epoch sits at a fixed place
+// in the workspace header, every block reads it at its start, and the call's
+// vote launch -- the next kernel on the stream, so every k_front block has
+// read it -- advances it (VoteArgs::front_epoch), so a flag the previous call
+// left never carries this call's tag.  (A CAS ticket electing k_front's last
+// block to do it cost ~150 us per call: 150 blocks retrying on one address.)  A flag not seen
+// within kLookbackSpin (its block not yet dispatched) is worked out by the
+// waiting thread from the mask itself: every wait ends, and no dispatch
+// order is assumed.  Replaces k_fg_count + k_compact for grids of at most
+// PVV_FRONT_MAX blocks (one launch and ~8x fewer blocks per image: the two
+// small kernels' 2,400 blocks per frame cost the batch-1 stream ~9 ms per
+// 1,024 frames of GPU time, profiles/r06/ablation.txt).
+// ==========================================================================
+#ifndef PVV_FRONT
+#define PVV_FRONT 0          // measured slower in the stream: kept for A/B
+#endif
+#ifndef PVV_FRONT_MAX
+#define PVV_FRONT_MAX 1024   // blocks (b x ceil(P / kFrontPx)) up to which k_front runs
+#endif
+struct FrontArgs {
+    MaskView m;
+    VertexView vx;
+    int H, W, vn, nfb, min_num, max_num;
+    uint64_t seed;
+    const uint8_t *keep;
+    uint64_t *hdr, *flag, *bal;
+    int32_t *tn, *fgtot;
+    float4 *pex;
+    int32_t *zero;
+    int64_t zero_words;
+};
+
+// block j's (kept) foreground count worked out from the mask: the fallback
+// when its flag does not show up in time (slow; pathological schedules only)
+template <int KIND, bool EVD>
+__device__ int front_self_count(const FrontArgs &a, int b, int j, bool kept, int fgb) {
+    const int64_t P = (int64_t)a.H * a.W;
+    int n = 0;
+    for (int i = 0; i < kFrontPx; ++i) {
+        const int64_t p = (int64_t)j * kFrontPx + i;
+        if (p >= P) break;
+        const int r = (int)(p / a.W), c = (int)(p - (int64_t)r * a.W);
+        bool f = is_fg<KIND, EVD>(a.m, b, r, c);
+        if (f && kept)
+            f = a.keep ? a.keep[b * P + p] != 0 : rand_unit(a.seed, (uint64_t)b * P + p) < (float)a.max_num / (float)fgb;
+        n += f;
+    }
+    return n;
+}
+
+// a flag is {52 bits of mix64(epoch + 1), 12-bit count}: the workspace's
+// first call finds whatever the memory held (often small integers, e.g. an
+// earlier workspace's vote counts), which a plain epoch number could match;
+// a hashed tag matches such garbage with probability 2^-52
+constexpr uint64_t kFrontCntMask = 0xFFFull;
+__device__ __forceinline__ uint64_t front_tag(uint64_t epoch1) { return mix64(epoch1 ^ 0x6a09e667f3bcc909ull); }
+#ifdef PVV_FRONT_STATS
+__device__ unsigned long long g_fstat[4];   // debug builds: fallbacks, spin rounds, max wait (ticks), blocks
+#endif
+
+// sum over a k_front block of (x, y); `sh` holds >= 2 kFrontNW ints
+__device__ __forceinline__ int2 front_sum2(int x, int y, int *sh) {
+    x = wave_sum_i(x);
+    y = wave_sum_i(y);
+    __syncthreads();
+    if (lane_id() == 0) { sh[threadIdx.x / 64] = x; sh[kFrontNW + threadIdx.x / 64] = y; }
+    __syncthreads();
+    int2 r = make_int2(0, 0);
+#pragma unroll
+    for (int w = 0; w < kFrontNW; ++w) { r.x += sh[w]; r.y += sh[kFrontNW + w]; }
+    return r;
+}
+
+// the all-gather of round `rnd`: (image total, sum of the blocks before blk)
+template <int KIND, bool EVD>
+__device__ __forceinline__ int2 front_gather(const FrontArgs &a, int b, int blk, uint64_t tag, int rnd, int own,
+                                             int fgb, int *sh) {
+    const uint64_t *fl = a.flag + ((int64_t)rnd * gridDim.y + b) * a.nfb;
+    int all = 0, pre = 0;
+    const uint64_t t_dead = __builtin_amdgcn_s_memrealtime() + kLookbackSpin;
+    for (int j = threadIdx.x; j < a.nfb; j += kFrontT) {
+        int c;
+        if (j == blk) {
+            c = own;
+        } else if (g_lb_self) {   // test hook: every count worked out by the waiter
+            c = front_self_count<KIND, EVD>(a, b, j, rnd == 1, fgb);
+        } else {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            uint64_t fv = ld_agent(&fl[j]);
+            int spins = 0;
+            while ((fv & ~kFrontCntMask) != tag && __builtin_amdgcn_s_memrealtime() < t_dead) {
+                __builtin_amdgcn_s_sleep(1);
+                fv = ld_agent(&fl[j]);
+                ++spins;
+            }
+            const bool ok = (fv & ~kFrontCntMask) == tag && (fv & kFrontCntMask) <= (uint64_t)kFrontPx;
+            c = ok ? (int)(fv & kFrontCntMask) : front_self_count<KIND, EVD>(a, b, j, rnd == 1, fgb);
+#ifdef PVV_FRONT_STATS
+            if (!ok) atomicAdd(&g_fstat[0], 1ull);
+            if (spins) atomicAdd(&g_fstat[1], (unsigned long long)spins);
+            atomicMax(&g_fstat[2], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - t0));
+#else
+            (void)t0; (void)spins;
+#endif
+        }
+        all += c;
+        pre += j < blk ? c : 0;
+    }
+    return front_sum2(all, pre, sh);
+}
+
+template <int KIND, bool EVD, int VK>
+__global__ __launch_bounds__(kFrontT) void k_front(FrontArgs a) {
+    const int b = (int)blockIdx.y, blk = (int)blockIdx.x;
+    const int wid = (int)threadIdx.x / 64, lane = lane_id();
+    const int64_t P = (int64_t)a.H * a.W;
+    __shared__ int sh[2 * kFrontNW];
+    __shared__ int wc[kFrontWords + 1];
+    __shared__ uint32_t pos[kFrontPx];   // the block's kept pixels in rank order: col | row << 16
+    {   // zero the pipeline's counters and hand-off granules (read only by later kernels)
+        const int64_t g = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kFrontT + threadIdx.x;
+        const int64_t G = (int64_t)gridDim.x * gridDim.y * kFrontT;
+        for (int64_t i = g; i < a.zero_words; i += G) a.zero[i] = 0;
+    }
+    const uint64_t epoch1 = ld_agent(&a.hdr[0]) + 1u;
+#ifdef PVV_FRONT_STATS
+    if (threadIdx.x == 0) atomicAdd(&g_fstat[3], 1ull);
+#endif
+    // ---- 1. foreground of pixels p0 + kFrontT k: every load in range (clamped),
+    // none behind a branch, so the block's mask reads are one round trip
+    const int64_t p0 = (int64_t)blk * kFrontPx + threadIdx.x;
+    int rk[kFrontK], ck[kFrontK];
+    bool f[kFrontK];
+    {
+        const int64_t q = min(p0, P - 1);
+        int r = (int)(q / a.W), c = (int)(q - (int64_t)r * a.W);
+#pragma unroll
+        for (int k = 0; k < kFrontK; ++k) {
+            const bool in = p0 + kFrontT * k < P;
+            rk[k] = in ? r : (int)((P - 1) / a.W);
+            ck[k] = in ? c : (int)(P - 1 - (int64_t)rk[k] * a.W);
+            c += kFrontT;
+            while (c >= a.W) { c -= a.W; ++r; }
+        }
+#pragma unroll
+        for (int k = 0; k < kFrontK; ++k) f[k] = is_fg<KIND, EVD>(a.m, b, rk[k], ck[k]);
+#pragma unroll
+        for (int k = 0; k < kFrontK; ++k) f[k] = f[k] && p0 + kFrontT * k < P;
+    }
+    const uint64_t tag = front_tag(epoch1) & ~kFrontCntMask;
+    uint64_t *bal = a.bal + ((int64_t)b * a.nfb + blk) * kFrontWords;
+    // the block's ballots (k-major: row-major pixel order) stored, then its
+    // count published; wc[] becomes each ballot's exclusive offset
+    auto publish = [&](int rnd, uint64_t (&bw)[kFrontK]) -> int {
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < kFrontK; ++k) {
+                st_agent(&bal[k * kFrontNW + wid], bw[k]);
+                wc[k * kFrontNW + wid] = __popcll(bw[k]);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int run = 0;
+            for (int i = 0; i < kFrontWords; ++i) { const int x = wc[i]; wc[i] = run; run += x; }
+            wc[kFrontWords] = run;
+            st_agent(&a.flag[((int64_t)rnd * gridDim.y + b) * a.nfb + blk], tag | (uint64_t)run);
+        }
+        __syncthreads();
+        return wc[kFrontWords];
+    };
+    uint64_t bw[kFrontK];
+#pragma unroll
+    for (int k = 0; k < kFrontK; ++k) bw[k] = ballot(f[k]);
+    const int own = publish(0, bw);
+    // ---- 2. the image's total and this block's offset
+    const int2 tot = front_gather<KIND, EVD>(a, b, blk, tag, 0, own, 0, sh);
+    const int fgb = tot.x;
+    if (fgb < a.min_num) {
+        if (blk == 0 && threadIdx.x == 0) { a.tn[b] = 0; a.fgtot[b] = fgb; }
+        return;
+    }
+    int base = tot.y, nsel = own, total = fgb;
+    if (fgb > a.max_num) {
+        // ---- 3. Bernoulli(max_num / fg) downsampling, then the kept pixels' round
+        const float pk = (float)a.max_num / (float)fgb;
+#pragma unroll
+        for (int k = 0; k < kFrontK; ++k) {
+            const int64_t p = p0 + kFrontT * k;
+            if (f[k]) f[k] = a.keep ? a.keep[b * P + p] != 0 : rand_unit(a.seed, (uint64_t)b * P + p) < pk;
+            bw[k] = ballot(f[k]);
+        }
+        nsel = publish(1, bw);
+        const int2 t2 = front_gather<KIND, EVD>(a, b, blk, tag, 1, nsel, fgb, sh);
+        total = t2.x;
+        base = t2.y;
+    }
+    if (blk == 0 && threadIdx.x == 0) { a.tn[b] = total; a.fgtot[b] = fgb; }
+    // ---- 4. the kept pixels in rank order, then their records: task i =
+    // (keypoint i / nsel, pixel i % nsel), all of a thread's tasks' loads in
+    // flight together (up to kFrontU; ~600 kept pixels x 9 keypoints per block
+    // of an object's interior is 11 tasks per thread)
+#pragma unroll
+    for (int k = 0; k < kFrontK; ++k)
+        if (f[k]) {
+            const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bw[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bw[k], 0));
+            pos[wc[k * kFrontNW + wid] + below] = (uint32_t)ck[k] | ((uint32_t)rk[k] << 16);
+        }
+    __syncthreads();
+    constexpr int ES = VK == PV_VERTEX_F32 ? 4 : 2;
+    const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)((const char *)a.vx.p + (int64_t)b * a.vx.s[0] * ES), (short)0, a.vx.extent, 0x00020000);
+    const int s4 = uniform((int)(a.vx.s[4] * ES));
+    const int s1 = (int)(a.vx.s[1] * ES), s2 = (int)(a.vx.s[2] * ES), s3 = (int)(a.vx.s[3] * ES);
+    float4 *eb = a.pex + (int64_t)b * a.vn * P + base;
+    const int n = nsel * a.vn;
+    constexpr int U = 12;
+    // (v, k) of task threadIdx.x, advanced by kFrontT tasks per step without a division
+    int v = 0, k = (int)threadIdx.x;
+    while (k >= nsel && v < a.vn) { k -= nsel; ++v; }
+    for (int i0 = (int)threadIdx.x; i0 < n; i0 += kFrontT * U) {
+        float x[U], y[U];
+        uint32_t pk_[U];
+        int vv[U], kk[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool ok = i0 + kFrontT * u < n;
+            vv[u] = ok ? v : 0;
+            kk[u] = ok ? k : 0;
+            pk_[u] = pos[kk[u]];
+            const int vo = (int)(pk_[u] >> 16) * s1 + (int)(pk_[u] & 0xffffu) * s2 + vv[u] * s3;
+            if constexpr (VK == PV_VERTEX_F32) {
+                x[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vr, vo, 0, 0));
+                y[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vr, vo, s4, 0));
+            } else {
+                x[u] = __half2float(__ushort_as_half(__builtin_amdgcn_raw_buffer_load_b16(vr, vo, 0, 0)));
+                y[u] = __half2float(__ushort_as_half(__builtin_amdgcn_raw_buffer_load_b16(vr, vo, s4, 0)));
+            }
+            k += kFrontT;
+            while (k >= nsel && v < a.vn) { k -= nsel; ++v; }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t t = (int64_t)base + kk[u];
+            if (i0 + kFrontT * u < n && t < P)
+                eb[(int64_t)vv[u] * P + kk[u]] =
+                    make_float4((float)(pk_[u] & 0xffffu), (float)(pk_[u] >> 16), x[u], y[u]);
+        }
+    }
 }
 
 // ==========================================================================
@@ -701,6 +1189,7 @@ struct VoteArgs {
     float thr, tau, gzf, gzr;
     uint64_t *trace;            // debug: per-wave (start, end) s_memrealtime stamps, or nullptr
     int32_t rw[4];              // SH, four resident rounds of blocks: work weights per round (0: even)
+    uint64_t *front_epoch;      // k_front's epoch, advanced by block 0 (the call's first vote launch), or nullptr
 };
 
 // Share of unit w when the units come in four dispatch rounds of B = n / 4
@@ -1313,6 +1802,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     const int64_t nunits = SH ? (int64_t)gridDim.x : (int64_t)gridDim.x * 4;
     const int gpu = SH ? 4 : 1;           // hypothesis groups per unit
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    if (a.front_epoch && blockIdx.x == 0 && threadIdx.x == 0) *a.front_epoch += 1;
     // the prologue (hypotheses, first sub-chunk) at the top issue priority:
     // the hot loops rank 0..2 by the work they have left (set_prio), and a
     // wave still in its prologue would otherwise wait behind them
@@ -1371,6 +1861,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
 // (image, hypothesis, keypoint): the pixel pair (the caller's idxs or the
 // counter RNG, RV:553) and its intersection (KU:11-49), stored in the
 // reference layout and keypoint-major; images without a vote are left alone.
+// profiling ablations only (pv_debug_set_ablation bit 32): a launch that does nothing
+__global__ void k_abl_empty(int) {}
+
 __global__ __launch_bounds__(256) void k_hyp_gen(VoteArgs a) {
     const int64_t per = (int64_t)a.nh * a.vn;
     const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1474,6 +1967,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
     const int unit = (int)blockIdx.x;
     const uint32_t nunits = gridDim.x;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    if (a.front_epoch && unit == 0 && threadIdx.x == 0) *a.front_epoch += 1;
     __builtin_amdgcn_s_setprio(3);
     __shared__ MSlab<PREPPED> slab[2];
     __shared__ QuarterBoxes qb_all[2];
@@ -3321,11 +3815,19 @@ uint64_t *g_vote_trace = nullptr;   // trace builds only (pv_debug_set_vote_trac
 // (pvnet_amd/build.py; pv_build_config() reports them): no environment
 // variable changes what the library runs.  The A/B measurements behind each
 // default are in the comments and DESIGN.md section 7.
+#ifndef PVV_ABL
+#define PVV_ABL 0           // profiling ablations only (outputs wrong): 1 no k_compact, 2 no k_hyp_gen, 4 no vote, 8 no refine, 16 no k_fg_count
+#endif
+// the ablation bits in effect (pv_debug_set_ablation; set between captures by profiling tools only)
+int g_abl = PVV_ABL;
 #ifndef PVV_VM_BPC
 #define PVV_VM_BPC 3        // k_vote_mfma blocks per CU (tools/vm_ab.sh, 8 in flight: 4 -> 36.6k images/s, 3 -> 40.2k, 2 -> 39.7k)
 #endif
 #ifndef PVV_HYPGEN
 #define PVV_HYPGEN 1        // hypotheses by k_hyp_gen before the vote: 34.6k -> 36.6k images/s, vote 35.2 -> 31.8 us
+#endif
+#ifndef PVV_HYPFUSE
+#define PVV_HYPFUSE 1       // ... made by k_compact's first blocks instead of a k_hyp_gen launch (round 6)
 #endif
 #ifndef PVV_BYTES_XCD
 #define PVV_BYTES_XCD 1     // k_vote_bytes: XCD-contiguous item ranges (31.1 vs 31.9 us interleaved)
@@ -3394,6 +3896,12 @@ struct Launch {
     bool evd;
 };
 
+int front_blocks(int H, int W) { return (int)(((int64_t)H * W + kFrontPx - 1) / kFrontPx); }
+// does the compaction run as k_front (which needs the vote launch after it to advance its epoch)?
+bool front_used(int b, int H, int W) {
+    return PVV_FRONT && (int64_t)front_blocks(H, W) * b <= PVV_FRONT_MAX && !(g_abl & 1) && !(g_abl & 4);
+}
+
 template <template <int, bool> class F, typename... A>
 int dispatch_mask(int kind, bool evd, A... args) {
     switch (kind) {
@@ -3418,40 +3926,59 @@ struct CompactArgs {
     uint64_t seed;
     const uint8_t *keep;
     Workspace ws;
+    HypGen hg;          // hg.nhb > 0: k_compact's first blocks make the hypotheses
     hipStream_t s;
 };
 
 template <int KIND, bool EVD>
 struct CompactStage {
     static int run(const CompactArgs *a) {
-        dim3 grid(a->nblk, a->b);
+        const int nfb = front_blocks(a->H, a->W);
+        if (front_used(a->b, a->H, a->W)) {
+            FrontArgs f{};
+            f.m = a->m; f.vx = a->vx;
+            f.H = a->H; f.W = a->W; f.vn = a->vn; f.nfb = nfb;
+            f.min_num = a->min_num; f.max_num = a->max_num;
+            f.seed = a->seed; f.keep = a->keep;
+            f.hdr = a->ws.fhdr; f.flag = a->ws.fflag; f.bal = a->ws.fbal;
+            f.tn = a->ws.tn; f.fgtot = a->ws.fgtot; f.pex = a->ws.pex;
+            f.zero = a->ws.counts; f.zero_words = a->ws.zero_words;
+            if (a->vx.kind == PV_VERTEX_F32)
+                k_front<KIND, EVD, PV_VERTEX_F32><<<dim3(nfb, a->b), kFrontT, 0, a->s>>>(f);
+            else
+                k_front<KIND, EVD, PV_VERTEX_F16><<<dim3(nfb, a->b), kFrontT, 0, a->s>>>(f);
+            return last();
+        }
+        dim3 grid(a->nblk + a->hg.nhb, a->b);
         static_assert(kFgWideCPB == 8, "grpcnt: groups of 8 chunks");
-        if ((int64_t)a->nblk * a->b > kFgWideAbove)
+        if (g_abl & 16) {
+        } else if ((int64_t)a->nblk * a->b > kFgWideAbove)
             k_fg_count<KIND, EVD, kFgWideCPB><<<dim3((a->nblk + kFgWideCPB - 1) / kFgWideCPB, a->b), 256, 0, a->s>>>(
                 a->m, a->H, a->W, a->ws.blkcnt, a->ws.fgbits, a->ws.grpcnt, a->nblk, a->ws.counts, a->ws.zero_words);
         else
             k_fg_count<KIND, EVD, 1><<<dim3(a->nblk, a->b), 256, 0, a->s>>>(a->m, a->H, a->W, a->ws.blkcnt, a->ws.fgbits,
                                                                           nullptr, a->nblk, a->ws.counts,
                                                                           a->ws.zero_words);
+        if (g_abl & 1) return last();
         if ((int64_t)a->nblk * a->b > kFgWideAbove) {
             if (a->vx.kind == PV_VERTEX_F32)
                 k_compact<KIND, EVD, PV_VERTEX_F32, true><<<grid, 256, 0, a->s>>>(
                     a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.grpcnt, a->ws.fgbits, a->ws.dsagg, a->nblk, a->min_num,
-                    a->max_num, a->seed, a->keep, a->ws.tn, a->ws.fgtot, a->ws.pex);
+                    a->max_num, a->seed, a->keep, a->ws.tn, a->ws.fgtot, a->ws.pex, a->hg);
             else
                 k_compact<KIND, EVD, PV_VERTEX_F16, true><<<grid, 256, 0, a->s>>>(
                     a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.grpcnt, a->ws.fgbits, a->ws.dsagg, a->nblk, a->min_num,
-                    a->max_num, a->seed, a->keep, a->ws.tn, a->ws.fgtot, a->ws.pex);
+                    a->max_num, a->seed, a->keep, a->ws.tn, a->ws.fgtot, a->ws.pex, a->hg);
             return last();
         }
         if (a->vx.kind == PV_VERTEX_F32)
             k_compact<KIND, EVD, PV_VERTEX_F32, false><<<grid, 256, 0, a->s>>>(a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.grpcnt, a->ws.fgbits, a->ws.dsagg,
                                                      a->nblk, a->min_num, a->max_num, a->seed, a->keep, a->ws.tn,
-                                                     a->ws.fgtot, a->ws.pex);
+                                                     a->ws.fgtot, a->ws.pex, a->hg);
         else
             k_compact<KIND, EVD, PV_VERTEX_F16, false><<<grid, 256, 0, a->s>>>(a->m, a->vx, a->H, a->W, a->vn, a->ws.blkcnt, a->ws.grpcnt, a->ws.fgbits, a->ws.dsagg,
                                                      a->nblk, a->min_num, a->max_num, a->seed, a->keep, a->ws.tn,
-                                                     a->ws.fgtot, a->ws.pex);
+                                                     a->ws.fgtot, a->ws.pex, a->hg);
         return last();
     }
 };
@@ -3494,6 +4021,20 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
     ca.keep = prm->keep;
     ca.ws = w;
     ca.s = s;
+    // every check that could fail comes before the compaction: once k_front
+    // ran, the vote launch must follow (it advances k_front's epoch)
+    if ((int64_t)vn * ((nh + kGroup - 1) / kGroup) * P >= (1ll << 31)) return PV_EINVAL;
+    const bool fr = front_used(b, H, W);
+    // the hypotheses by k_compact's first blocks (compact_hyp) instead of a k_hyp_gen launch
+    const bool hfuse = PVV_HYPFUSE && hyp_pregen_used(vn, nh) && !fr && nblk <= kHypMaxChunks && !(g_abl & 2);
+    ca.hg = HypGen{};
+    if (hfuse) {
+        ca.hg.nhb = (int)(((int64_t)nh * vn + 255) / 256);
+        ca.hg.nh = nh; ca.hg.vn = vn; ca.hg.min_num = prm->min_num; ca.hg.max_num = prm->max_num;
+        ca.hg.seed = mix64(prm->seed); ca.hg.kseed = ca.seed;
+        ca.hg.idxs = prm->idxs; ca.hg.keep = prm->keep;
+        ca.hg.hyp_out = w.hyp; ca.hg.hypv_out = w.hypv; ca.hg.diag_hyp = dg.hyp;
+    }
     int r = dispatch_mask<CompactStage>(img->mask_kind, evd, (const CompactArgs *)&ca);
     if (r) return r;
     if (dg.ev_compact_end) {
@@ -3519,7 +4060,9 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
     if (hyp_pregen_used(vn, nh)) {
         va.hypv_out = w.hypv;
         const int64_t nt = (int64_t)b * nh * vn;
-        k_hyp_gen<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(va);
+        if (hfuse) {
+        } else if (!(g_abl & 2)) k_hyp_gen<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(va);
+        else if (g_abl & 32) k_abl_empty<<<1, 64, 0, s>>>(0);
         if ((r = last())) return r;
         va.hyp = w.hypv; va.hyp_sb = (int64_t)vn * nh; va.hyp_sv = nh; va.hyp_sh = 1;
     }
@@ -3544,7 +4087,8 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
         if (vc.idxs) vc.idxs += (int64_t)b0 * nh * vn * 2;
         vc.counts += (int64_t)b0 * va.cnt_bs;
         vc.tn_dev += b0;
-        launch_vote<true>(vc, nb * per_img, s);
+        vc.front_epoch = fr && b0 == 0 ? w.fhdr : nullptr;
+        if (!(g_abl & 4)) launch_vote<true>(vc, nb * per_img, s);
         if ((r = last())) return r;
     }
     if (dg.ev_vote_end) return rc(hipEventRecord((hipEvent_t)dg.ev_vote_end, s));
@@ -3741,6 +4285,28 @@ int pv_debug_lookback_self(int32_t on) {
     return rc(hipMemcpyToSymbol(HIP_SYMBOL(g_lb_self), &on, sizeof(on)));
 }
 
+// debug only (profiling tools, never during a capture): pipeline kernels left out of the next
+// launches (bits: 1 k_compact, 2 k_hyp_gen, 4 vote, 8 refine, 16 k_fg_count; 32 with 2: an empty
+// kernel in k_hyp_gen's place); outputs are wrong
+int pv_debug_set_ablation(int32_t m) {
+    g_abl = m;
+    return PV_OK;
+}
+
+// debug only: k_front's hand-off statistics since the last call (PVV_FRONT_STATS builds):
+// out[0] flags worked out by the waiter, [1] spin rounds, [2] longest wait (10 ns ticks), [3] blocks
+int pv_debug_front_stats(uint64_t *out) {
+#ifdef PVV_FRONT_STATS
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fstat), 4 * sizeof(uint64_t));
+    if (e != hipSuccess) return rc(e);
+    const uint64_t z[4] = {0, 0, 0, 0};
+    return rc(hipMemcpyToSymbol(HIP_SYMBOL(g_fstat), z, sizeof(z)));
+#else
+    (void)out;
+    return PV_EINVAL;
+#endif
+}
+
 #ifdef PVV_TRACE
 // trace builds only: per-wave timestamps of the next pipeline vote launches
 void pv_debug_set_vote_trace(uint64_t *buf) { g_vote_trace = buf; }
@@ -3793,7 +4359,7 @@ int pv_ransac_voting_v3(const pv_image_desc *img, const pv_vote_params *prm, flo
     // hypotheses keypoint-major when the pipeline pre-generated them (coalesced), else the reference layout
     const bool hv = hyp_pregen_used(vn, nh);
     auto *kref = nh > kRefineLdsHyp ? k_refine_solve<true> : k_refine_solve<false>;
-    kref<<<dim3(kRefineNJ, vn, b), kRT, 0, s>>>(w.counts, hv ? w.hypv : w.hyp, (int64_t)nh * vn,
+    if (!(g_abl & 8)) kref<<<dim3(kRefineNJ, vn, b), kRT, 0, s>>>(w.counts, hv ? w.hypv : w.hyp, (int64_t)nh * vn,
                                                           hv ? nh : 1, hv ? 1 : vn, w.pex, w.tn, P, vn, nh,
                                                           prm->inlier_thresh, w.refslot,
                                                           prm->confidence, prm->max_iter, out, dg);

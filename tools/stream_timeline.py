@@ -3,6 +3,13 @@
     python tools/stream_timeline.py run [steps]          # the headline stream (bench.run_stream), plain
     python tools/stream_timeline.py empty [steps]        # the same graph shape, n trivial kernels per frame
     python tools/stream_timeline.py --analyze trace.csv  # a rocprofv3 kernel trace of `run`
+    python tools/stream_timeline.py abl [steps] m1,m2,..  # `run` with pipeline kernels left out of the graph
+
+`abl` warms every lane up with the whole pipeline (so each lane's workspace
+holds a real frame's records, hypotheses and pixel count), then captures the
+graph with the kernels of mask m left out (pv_debug_set_ablation: 1 k_compact,
+2 k_hyp_gen, 4 vote, 8 refine, 16 k_fg_count): what the stream costs without
+them, on real data.
 
 `empty` replays graphs of the headline's shape (1,024 frames per replay, 8
 lanes forked from the capture stream and joined) whose frames are n = 1..5
@@ -71,6 +78,25 @@ def main():
     args = argparse.Namespace(per_step=1024, inflight=8, warmup=3, hn=512)
     dev = torch.device("cuda:0")
     torch.cuda.set_device(0)
+    if sys.argv[1] == "abl":
+        import ctypes
+        from pvnet_amd import _lib
+        L = _lib.load()
+        L.pv_debug_set_ablation.argtypes = [ctypes.c_int32]
+        segs, vers, kps, tn = bench.make_fields(0, 1, 64, dev)
+        orig = bench.new_graph
+        for m in [int(x) for x in sys.argv[3].split(",")]:
+            def ng(m=m):
+                L.pv_debug_set_ablation(m)
+                return orig()
+            bench.new_graph = ng
+            hs = {}
+            el, _, _, _, _ = bench.run_stream(args, 1, 0, dev, segs, vers, steps, 0, stats=hs)
+            L.pv_debug_set_ablation(0)
+            bench.new_graph = orig
+            print(f"abl {m:2d}: {steps * 1024 / el:.1f} images/s, {el / steps * 1e3:.3f} ms/step, host "
+                  f"{hs['host_replay_s'] / steps * 1e3:.3f} ms/replay", flush=True)
+        return
     if sys.argv[1] == "run":
         segs, vers, kps, tn = bench.make_fields(0, 1, 64, dev)
         hs = {}
