@@ -51,11 +51,6 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kCompactChunk = 256;           // pixels per compaction block (one per thread)
-constexpr int kFrontPx = 2048;               // pixels per k_front block
-constexpr int kFrontT = 512;                 // k_front block threads (8 waves, 4 pixels each)
-constexpr int kFrontNW = kFrontT / 64;
-constexpr int kFrontK = kFrontPx / kFrontT;
-constexpr int kFrontWords = kFrontPx / 64;   // wave ballots per k_front block
 constexpr int kVoteChunk = 256;              // pixels per LDS-staged sub-chunk of the vote waves
 // refine blocks per (image, keypoint); measured with the gathering hand-off
 // (tools/ab_libs.sh, two rounds, stream images/s and sequential latency):
@@ -229,9 +224,6 @@ __device__ __forceinline__ bool is_fg(const MaskView &m, int b, int r, int c) {
 // workspace
 // --------------------------------------------------------------------------
 struct Workspace {
-    uint64_t *fhdr;     // k_front's header at offset 0 of every workspace: [0] epoch (low 32 bits), [1] ticket
-    uint64_t *fflag;    // [2][b][nfb]   k_front's tagged count flags (all-gather; round 2: downsampled counts)
-    uint64_t *fbal;     // [b][nfb][32]  k_front's (kept) pixel ballots, published before the flags
     int32_t *counts;    // [b][vn][nh]   zeroed by k_fg_count
     uint4 *refslot;     // [b][vn][kRefineNJ][kRefineGran] zeroed by k_fg_count: k_refine_solve's tagged partials
     int32_t *dsagg;     // [b][nblk]     zeroed by k_fg_count: downsampled count + 1 per block (look-back)
@@ -255,13 +247,6 @@ Workspace carve(void *base, int b, int H, int W, int vn, int nh) {
     char *p = (char *)base;
     int64_t off = 0;
     auto take = [&](int64_t bytes) { char *q = p ? p + off : nullptr; off = align_up(off + bytes, 256); return q; };
-    // k_front's header and flags first: their place does not depend on the
-    // shape, so flags a call left are only ever read as flags (tagged by the
-    // header's epoch, which only grows) whatever shape the next call has
-    const int64_t nfb = (P + kFrontPx - 1) / kFrontPx;
-    w.fhdr = (uint64_t *)take(256);
-    w.fflag = (uint64_t *)take(16 * b * nfb);
-    w.fbal = (uint64_t *)take(8 * kFrontWords * b * nfb);
     const int64_t ncnt = align_up((int64_t)b * vn * nh, 4);            // refslot 16-B aligned
     const int64_t nslot = (int64_t)b * vn * kRefineNJ * kRefineGran;
     w.zero_words = ncnt + 4 * nslot + b * nblk + 2 * (int64_t)b * vn;
@@ -865,271 +850,6 @@ __global__ __launch_bounds__(256) void k_compact(MaskView, VertexView vx, int H,
 }
 
 // ==========================================================================
-// K1 + K2 in one launch (round 6): k_front, the compaction of a small batch
-// (RV:533-552) by fat blocks of kFrontPx pixels, 8 per thread.
-//  1. each block counts its foreground (mask, or seg_pred's argmax), stores
-//     its 32 wave ballots and publishes its count as a tagged flag
-//     {epoch + 1, count} (agent-scope stores, ballots first);
-//  2. each block reads every flag of its image -- an all-gather, not a serial
-//     look-back: one image's blocks run side by side -- and so knows the
-//     image's total and its own row-major offset;
-//  3. fg > max_num: keep decisions (RV:543-546), kept ballots, a second
-//     tagged round of the same form;
-//  4. the block's kept pixels' records, (pixel, keypoint) tasks spread over
-//     its threads (a block of the object's interior holds ~600 of them).
-// No state has to be zeroed between calls: the epoch sits at a fixed place
-// in the workspace header, every block reads it at its start, and the call's
-// vote launch -- the next kernel on the stream, so every k_front block has
-// read it -- advances it (VoteArgs::front_epoch), so a flag the previous call
-// left never carries this call's tag.  (A CAS ticket electing k_front's last
-// block to do it cost ~150 us per call: 150 blocks retrying on one address.)  A flag not seen
-// within kLookbackSpin (its block not yet dispatched) is worked out by the
-// waiting thread from the mask itself: every wait ends, and no dispatch
-// order is assumed.  Replaces k_fg_count + k_compact for grids of at most
-// PVV_FRONT_MAX blocks (one launch and ~8x fewer blocks per image: the two
-// small kernels' 2,400 blocks per frame cost the batch-1 stream ~9 ms per
-// 1,024 frames of GPU time, profiles/r06/ablation.txt).
-// ==========================================================================
-#ifndef PVV_FRONT
-#define PVV_FRONT 0          // measured slower in the stream: kept for A/B
-#endif
-#ifndef PVV_FRONT_MAX
-#define PVV_FRONT_MAX 1024   // blocks (b x ceil(P / kFrontPx)) up to which k_front runs
-#endif
-struct FrontArgs {
-    MaskView m;
-    VertexView vx;
-    int H, W, vn, nfb, min_num, max_num;
-    uint64_t seed;
-    const uint8_t *keep;
-    uint64_t *hdr, *flag, *bal;
-    int32_t *tn, *fgtot;
-    float4 *pex;
-    int32_t *zero;
-    int64_t zero_words;
-};
-
-// block j's (kept) foreground count worked out from the mask: the fallback
-// when its flag does not show up in time (slow; pathological schedules only)
-template <int KIND, bool EVD>
-__device__ int front_self_count(const FrontArgs &a, int b, int j, bool kept, int fgb) {
-    const int64_t P = (int64_t)a.H * a.W;
-    int n = 0;
-    for (int i = 0; i < kFrontPx; ++i) {
-        const int64_t p = (int64_t)j * kFrontPx + i;
-        if (p >= P) break;
-        const int r = (int)(p / a.W), c = (int)(p - (int64_t)r * a.W);
-        bool f = is_fg<KIND, EVD>(a.m, b, r, c);
-        if (f && kept)
-            f = a.keep ? a.keep[b * P + p] != 0 : rand_unit(a.seed, (uint64_t)b * P + p) < (float)a.max_num / (float)fgb;
-        n += f;
-    }
-    return n;
-}
-
-// a flag is {52 bits of mix64(epoch + 1), 12-bit count}: the workspace's
-// first call finds whatever the memory held (often small integers, e.g. an
-// earlier workspace's vote counts), which a plain epoch number could match;
-// a hashed tag matches such garbage with probability 2^-52
-constexpr uint64_t kFrontCntMask = 0xFFFull;
-__device__ __forceinline__ uint64_t front_tag(uint64_t epoch1) { return mix64(epoch1 ^ 0x6a09e667f3bcc909ull); }
-#ifdef PVV_FRONT_STATS
-__device__ unsigned long long g_fstat[4];   // debug builds: fallbacks, spin rounds, max wait (ticks), blocks
-#endif
-
-// sum over a k_front block of (x, y); `sh` holds >= 2 kFrontNW ints
-__device__ __forceinline__ int2 front_sum2(int x, int y, int *sh) {
-    x = wave_sum_i(x);
-    y = wave_sum_i(y);
-    __syncthreads();
-    if (lane_id() == 0) { sh[threadIdx.x / 64] = x; sh[kFrontNW + threadIdx.x / 64] = y; }
-    __syncthreads();
-    int2 r = make_int2(0, 0);
-#pragma unroll
-    for (int w = 0; w < kFrontNW; ++w) { r.x += sh[w]; r.y += sh[kFrontNW + w]; }
-    return r;
-}
-
-// the all-gather of round `rnd`: (image total, sum of the blocks before blk)
-template <int KIND, bool EVD>
-__device__ __forceinline__ int2 front_gather(const FrontArgs &a, int b, int blk, uint64_t tag, int rnd, int own,
-                                             int fgb, int *sh) {
-    const uint64_t *fl = a.flag + ((int64_t)rnd * gridDim.y + b) * a.nfb;
-    int all = 0, pre = 0;
-    const uint64_t t_dead = __builtin_amdgcn_s_memrealtime() + kLookbackSpin;
-    for (int j = threadIdx.x; j < a.nfb; j += kFrontT) {
-        int c;
-        if (j == blk) {
-            c = own;
-        } else if (g_lb_self) {   // test hook: every count worked out by the waiter
-            c = front_self_count<KIND, EVD>(a, b, j, rnd == 1, fgb);
-        } else {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            uint64_t fv = ld_agent(&fl[j]);
-            int spins = 0;
-            while ((fv & ~kFrontCntMask) != tag && __builtin_amdgcn_s_memrealtime() < t_dead) {
-                __builtin_amdgcn_s_sleep(1);
-                fv = ld_agent(&fl[j]);
-                ++spins;
-            }
-            const bool ok = (fv & ~kFrontCntMask) == tag && (fv & kFrontCntMask) <= (uint64_t)kFrontPx;
-            c = ok ? (int)(fv & kFrontCntMask) : front_self_count<KIND, EVD>(a, b, j, rnd == 1, fgb);
-#ifdef PVV_FRONT_STATS
-            if (!ok) atomicAdd(&g_fstat[0], 1ull);
-            if (spins) atomicAdd(&g_fstat[1], (unsigned long long)spins);
-            atomicMax(&g_fstat[2], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - t0));
-#else
-            (void)t0; (void)spins;
-#endif
-        }
-        all += c;
-        pre += j < blk ? c : 0;
-    }
-    return front_sum2(all, pre, sh);
-}
-
-template <int KIND, bool EVD, int VK>
-__global__ __launch_bounds__(kFrontT) void k_front(FrontArgs a) {
-    const int b = (int)blockIdx.y, blk = (int)blockIdx.x;
-    const int wid = (int)threadIdx.x / 64, lane = lane_id();
-    const int64_t P = (int64_t)a.H * a.W;
-    __shared__ int sh[2 * kFrontNW];
-    __shared__ int wc[kFrontWords + 1];
-    __shared__ uint32_t pos[kFrontPx];   // the block's kept pixels in rank order: col | row << 16
-    {   // zero the pipeline's counters and hand-off granules (read only by later kernels)
-        const int64_t g = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kFrontT + threadIdx.x;
-        const int64_t G = (int64_t)gridDim.x * gridDim.y * kFrontT;
-        for (int64_t i = g; i < a.zero_words; i += G) a.zero[i] = 0;
-    }
-    const uint64_t epoch1 = ld_agent(&a.hdr[0]) + 1u;
-#ifdef PVV_FRONT_STATS
-    if (threadIdx.x == 0) atomicAdd(&g_fstat[3], 1ull);
-#endif
-    // ---- 1. foreground of pixels p0 + kFrontT k: every load in range (clamped),
-    // none behind a branch, so the block's mask reads are one round trip
-    const int64_t p0 = (int64_t)blk * kFrontPx + threadIdx.x;
-    int rk[kFrontK], ck[kFrontK];
-    bool f[kFrontK];
-    {
-        const int64_t q = min(p0, P - 1);
-        int r = (int)(q / a.W), c = (int)(q - (int64_t)r * a.W);
-#pragma unroll
-        for (int k = 0; k < kFrontK; ++k) {
-            const bool in = p0 + kFrontT * k < P;
-            rk[k] = in ? r : (int)((P - 1) / a.W);
-            ck[k] = in ? c : (int)(P - 1 - (int64_t)rk[k] * a.W);
-            c += kFrontT;
-            while (c >= a.W) { c -= a.W; ++r; }
-        }
-#pragma unroll
-        for (int k = 0; k < kFrontK; ++k) f[k] = is_fg<KIND, EVD>(a.m, b, rk[k], ck[k]);
-#pragma unroll
-        for (int k = 0; k < kFrontK; ++k) f[k] = f[k] && p0 + kFrontT * k < P;
-    }
-    const uint64_t tag = front_tag(epoch1) & ~kFrontCntMask;
-    uint64_t *bal = a.bal + ((int64_t)b * a.nfb + blk) * kFrontWords;
-    // the block's ballots (k-major: row-major pixel order) stored, then its
-    // count published; wc[] becomes each ballot's exclusive offset
-    auto publish = [&](int rnd, uint64_t (&bw)[kFrontK]) -> int {
-        if (lane == 0) {
-#pragma unroll
-            for (int k = 0; k < kFrontK; ++k) {
-                st_agent(&bal[k * kFrontNW + wid], bw[k]);
-                wc[k * kFrontNW + wid] = __popcll(bw[k]);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int run = 0;
-            for (int i = 0; i < kFrontWords; ++i) { const int x = wc[i]; wc[i] = run; run += x; }
-            wc[kFrontWords] = run;
-            st_agent(&a.flag[((int64_t)rnd * gridDim.y + b) * a.nfb + blk], tag | (uint64_t)run);
-        }
-        __syncthreads();
-        return wc[kFrontWords];
-    };
-    uint64_t bw[kFrontK];
-#pragma unroll
-    for (int k = 0; k < kFrontK; ++k) bw[k] = ballot(f[k]);
-    const int own = publish(0, bw);
-    // ---- 2. the image's total and this block's offset
-    const int2 tot = front_gather<KIND, EVD>(a, b, blk, tag, 0, own, 0, sh);
-    const int fgb = tot.x;
-    if (fgb < a.min_num) {
-        if (blk == 0 && threadIdx.x == 0) { a.tn[b] = 0; a.fgtot[b] = fgb; }
-        return;
-    }
-    int base = tot.y, nsel = own, total = fgb;
-    if (fgb > a.max_num) {
-        // ---- 3. Bernoulli(max_num / fg) downsampling, then the kept pixels' round
-        const float pk = (float)a.max_num / (float)fgb;
-#pragma unroll
-        for (int k = 0; k < kFrontK; ++k) {
-            const int64_t p = p0 + kFrontT * k;
-            if (f[k]) f[k] = a.keep ? a.keep[b * P + p] != 0 : rand_unit(a.seed, (uint64_t)b * P + p) < pk;
-            bw[k] = ballot(f[k]);
-        }
-        nsel = publish(1, bw);
-        const int2 t2 = front_gather<KIND, EVD>(a, b, blk, tag, 1, nsel, fgb, sh);
-        total = t2.x;
-        base = t2.y;
-    }
-    if (blk == 0 && threadIdx.x == 0) { a.tn[b] = total; a.fgtot[b] = fgb; }
-    // ---- 4. the kept pixels in rank order, then their records: task i =
-    // (keypoint i / nsel, pixel i % nsel), all of a thread's tasks' loads in
-    // flight together (up to kFrontU; ~600 kept pixels x 9 keypoints per block
-    // of an object's interior is 11 tasks per thread)
-#pragma unroll
-    for (int k = 0; k < kFrontK; ++k)
-        if (f[k]) {
-            const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bw[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bw[k], 0));
-            pos[wc[k * kFrontNW + wid] + below] = (uint32_t)ck[k] | ((uint32_t)rk[k] << 16);
-        }
-    __syncthreads();
-    constexpr int ES = VK == PV_VERTEX_F32 ? 4 : 2;
-    const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)((const char *)a.vx.p + (int64_t)b * a.vx.s[0] * ES), (short)0, a.vx.extent, 0x00020000);
-    const int s4 = uniform((int)(a.vx.s[4] * ES));
-    const int s1 = (int)(a.vx.s[1] * ES), s2 = (int)(a.vx.s[2] * ES), s3 = (int)(a.vx.s[3] * ES);
-    float4 *eb = a.pex + (int64_t)b * a.vn * P + base;
-    const int n = nsel * a.vn;
-    constexpr int U = 12;
-    // (v, k) of task threadIdx.x, advanced by kFrontT tasks per step without a division
-    int v = 0, k = (int)threadIdx.x;
-    while (k >= nsel && v < a.vn) { k -= nsel; ++v; }
-    for (int i0 = (int)threadIdx.x; i0 < n; i0 += kFrontT * U) {
-        float x[U], y[U];
-        uint32_t pk_[U];
-        int vv[U], kk[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool ok = i0 + kFrontT * u < n;
-            vv[u] = ok ? v : 0;
-            kk[u] = ok ? k : 0;
-            pk_[u] = pos[kk[u]];
-            const int vo = (int)(pk_[u] >> 16) * s1 + (int)(pk_[u] & 0xffffu) * s2 + vv[u] * s3;
-            if constexpr (VK == PV_VERTEX_F32) {
-                x[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vr, vo, 0, 0));
-                y[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vr, vo, s4, 0));
-            } else {
-                x[u] = __half2float(__ushort_as_half(__builtin_amdgcn_raw_buffer_load_b16(vr, vo, 0, 0)));
-                y[u] = __half2float(__ushort_as_half(__builtin_amdgcn_raw_buffer_load_b16(vr, vo, s4, 0)));
-            }
-            k += kFrontT;
-            while (k >= nsel && v < a.vn) { k -= nsel; ++v; }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t t = (int64_t)base + kk[u];
-            if (i0 + kFrontT * u < n && t < P)
-                eb[(int64_t)vv[u] * P + kk[u]] =
-                    make_float4((float)(pk_[u] & 0xffffu), (float)(pk_[u] >> 16), x[u], y[u]);
-        }
-    }
-}
-
-// ==========================================================================
 // K4: hypotheses (KU:11-49) + fused vote/count.
 // counts[b][v][h] += #{t : inlier(h, v, t)}.
 //
@@ -1189,7 +909,6 @@ struct VoteArgs {
     float thr, tau, gzf, gzr;
     uint64_t *trace;            // debug: per-wave (start, end) s_memrealtime stamps, or nullptr
     int32_t rw[4];              // SH, four resident rounds of blocks: work weights per round (0: even)
-    uint64_t *front_epoch;      // k_front's epoch, advanced by block 0 (the call's first vote launch), or nullptr
 };
 
 // Share of unit w when the units come in four dispatch rounds of B = n / 4
@@ -1802,7 +1521,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     const int64_t nunits = SH ? (int64_t)gridDim.x : (int64_t)gridDim.x * 4;
     const int gpu = SH ? 4 : 1;           // hypothesis groups per unit
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    if (a.front_epoch && blockIdx.x == 0 && threadIdx.x == 0) *a.front_epoch += 1;
     // the prologue (hypotheses, first sub-chunk) at the top issue priority:
     // the hot loops rank 0..2 by the work they have left (set_prio), and a
     // wave still in its prologue would otherwise wait behind them
@@ -1967,7 +1685,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
     const int unit = (int)blockIdx.x;
     const uint32_t nunits = gridDim.x;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    if (a.front_epoch && unit == 0 && threadIdx.x == 0) *a.front_epoch += 1;
     __builtin_amdgcn_s_setprio(3);
     __shared__ MSlab<PREPPED> slab[2];
     __shared__ QuarterBoxes qb_all[2];
@@ -3896,11 +3613,6 @@ struct Launch {
     bool evd;
 };
 
-int front_blocks(int H, int W) { return (int)(((int64_t)H * W + kFrontPx - 1) / kFrontPx); }
-// does the compaction run as k_front (which needs the vote launch after it to advance its epoch)?
-bool front_used(int b, int H, int W) {
-    return PVV_FRONT && (int64_t)front_blocks(H, W) * b <= PVV_FRONT_MAX && !(g_abl & 1) && !(g_abl & 4);
-}
 
 template <template <int, bool> class F, typename... A>
 int dispatch_mask(int kind, bool evd, A... args) {
@@ -3933,22 +3645,6 @@ struct CompactArgs {
 template <int KIND, bool EVD>
 struct CompactStage {
     static int run(const CompactArgs *a) {
-        const int nfb = front_blocks(a->H, a->W);
-        if (front_used(a->b, a->H, a->W)) {
-            FrontArgs f{};
-            f.m = a->m; f.vx = a->vx;
-            f.H = a->H; f.W = a->W; f.vn = a->vn; f.nfb = nfb;
-            f.min_num = a->min_num; f.max_num = a->max_num;
-            f.seed = a->seed; f.keep = a->keep;
-            f.hdr = a->ws.fhdr; f.flag = a->ws.fflag; f.bal = a->ws.fbal;
-            f.tn = a->ws.tn; f.fgtot = a->ws.fgtot; f.pex = a->ws.pex;
-            f.zero = a->ws.counts; f.zero_words = a->ws.zero_words;
-            if (a->vx.kind == PV_VERTEX_F32)
-                k_front<KIND, EVD, PV_VERTEX_F32><<<dim3(nfb, a->b), kFrontT, 0, a->s>>>(f);
-            else
-                k_front<KIND, EVD, PV_VERTEX_F16><<<dim3(nfb, a->b), kFrontT, 0, a->s>>>(f);
-            return last();
-        }
         dim3 grid(a->nblk + a->hg.nhb, a->b);
         static_assert(kFgWideCPB == 8, "grpcnt: groups of 8 chunks");
         if (g_abl & 16) {
@@ -4021,12 +3717,9 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
     ca.keep = prm->keep;
     ca.ws = w;
     ca.s = s;
-    // every check that could fail comes before the compaction: once k_front
-    // ran, the vote launch must follow (it advances k_front's epoch)
     if ((int64_t)vn * ((nh + kGroup - 1) / kGroup) * P >= (1ll << 31)) return PV_EINVAL;
-    const bool fr = front_used(b, H, W);
     // the hypotheses by k_compact's first blocks (compact_hyp) instead of a k_hyp_gen launch
-    const bool hfuse = PVV_HYPFUSE && hyp_pregen_used(vn, nh) && !fr && nblk <= kHypMaxChunks && !(g_abl & 2);
+    const bool hfuse = PVV_HYPFUSE && hyp_pregen_used(vn, nh) && nblk <= kHypMaxChunks && !(g_abl & 2);
     ca.hg = HypGen{};
     if (hfuse) {
         ca.hg.nhb = (int)(((int64_t)nh * vn + 255) / 256);
@@ -4087,7 +3780,6 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
         if (vc.idxs) vc.idxs += (int64_t)b0 * nh * vn * 2;
         vc.counts += (int64_t)b0 * va.cnt_bs;
         vc.tn_dev += b0;
-        vc.front_epoch = fr && b0 == 0 ? w.fhdr : nullptr;
         if (!(g_abl & 4)) launch_vote<true>(vc, nb * per_img, s);
         if ((r = last())) return r;
     }
@@ -4291,20 +3983,6 @@ int pv_debug_lookback_self(int32_t on) {
 int pv_debug_set_ablation(int32_t m) {
     g_abl = m;
     return PV_OK;
-}
-
-// debug only: k_front's hand-off statistics since the last call (PVV_FRONT_STATS builds):
-// out[0] flags worked out by the waiter, [1] spin rounds, [2] longest wait (10 ns ticks), [3] blocks
-int pv_debug_front_stats(uint64_t *out) {
-#ifdef PVV_FRONT_STATS
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fstat), 4 * sizeof(uint64_t));
-    if (e != hipSuccess) return rc(e);
-    const uint64_t z[4] = {0, 0, 0, 0};
-    return rc(hipMemcpyToSymbol(HIP_SYMBOL(g_fstat), z, sizeof(z)));
-#else
-    (void)out;
-    return PV_EINVAL;
-#endif
 }
 
 #ifdef PVV_TRACE
