@@ -577,7 +577,7 @@ def main():
         raise SystemExit(f"keypoint error {err} px > 5 on the synthetic fields (tn={tn})")
 
     # the same stream with 4 consecutive resident frames per call (one batched
-    # v3 call: 5 kernel nodes per 4 frames instead of per frame): separates
+    # v3 call: its 4 kernel nodes per 4 frames instead of per frame): separates
     # the host's per-node graph submission from the GPU's work per frame
     sb = None
     if not args.skip_batched:
@@ -620,18 +620,25 @@ def main():
         dist.destroy_process_group()
 
 
+def kernel_nodes(frames_per_call=1, hn=512):
+    """Kernel launches (graph nodes) of one v3 call on frames_per_call
+    480x640 frames, as the library reports them (pv_v3_kernel_launches)."""
+    from pvnet_amd import _lib
+    return int(_lib.load().pv_v3_kernel_launches(frames_per_call, H, W, VN, hn))
+
+
 def stream_batched(args, ws, rank, dev, segs, vers, kps, f):
     """stream_batched<f>: the headline stream's frames, sharding, lanes and
     gather, but each lane call votes f consecutive resident frames as one
     batch (RV:531's per-image loop is batched in the reference's pipeline
-    too): 5 kernel nodes per f frames.  Not the headline (batch-1 frames)."""
+    too): one call's kernel nodes per f frames.  Not the headline (batch-1 frames)."""
     K, M, NF = args.steps, args.per_step, len(segs)
     hs = {}
     elapsed, local, _, _, _ = run_stream(args, ws, rank, dev, segs, vers, K, 77_000, frames_per_call=f, stats=hs)
     n = ws * K * M
     err = float(np.abs(local.cpu().numpy() - kps[np.arange(K * M) % NF]).max())
     return dict(images_per_s=round(n / elapsed, 1), ms_per_step=round(elapsed / K * 1e3, 4), steps=K,
-                frames_per_call=f, per_gpu_batch_per_step=M, kernel_nodes_per_frame=5.0 / f,
+                frames_per_call=f, per_gpu_batch_per_step=M, kernel_nodes_per_frame=kernel_nodes(f) / f,
                 host_ms_per_replay=round(hs["host_replay_s"] / K * 1e3, 4), max_kp_err_px=round(err, 4),
                 note="the headline stream (same fields, 8 lanes, one graph replay per %d frames) with %d consecutive "
                      "frames per ransac_voting_layer_v3 call; host_ms_per_replay = host time inside "
@@ -1342,6 +1349,7 @@ def report(args, ws, res, final_err, dev):
         "stream_order_ok": res["order_err"] <= 5.0,
         "latency_ms_per_image": round(res["latency_ms"], 5),
         "host_ms_per_replay": round(res["host_ms_per_replay"], 4),
+        "kernel_nodes_per_frame": kernel_nodes(1, args.hn),
         "rank_cpus": args.rank_cpus_all,
         "rank_cpus_source": args.rank_cpus[1],
         "library": library_config(),

@@ -140,6 +140,10 @@ typedef struct pv_v3_diag {
 } pv_v3_diag;
 
 size_t pv_v3_workspace_size(int32_t b, int32_t H, int32_t W, int32_t vn, int32_t n_hyp);
+/* Kernel launches one pv_ransac_voting_v3 call of this shape makes (the graph nodes it adds when
+ * captured): compaction (2), hypotheses (0 when k_compact makes them), vote (1 per 2^31-pair chunk),
+ * refine (1).  Build-internal (not in the reference API); 0 for an invalid shape. */
+int pv_v3_kernel_launches(int32_t b, int32_t H, int32_t W, int32_t vn, int32_t n_hyp);
 
 /* ransac_voting_layer_v3 (RV:520-604) for a whole batch; out f32 [b,vn,2]. */
 int pv_ransac_voting_v3(const pv_image_desc *img, const pv_vote_params *prm, float *out,

@@ -66,6 +66,7 @@ SIGNATURES = [
     ("pv_voting_for_hypothesis_vp", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp]),
     ("pv_vote_counts", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp]),
     ("pv_v3_workspace_size", c_size, [c_i32, c_i32, c_i32, c_i32, c_i32]),
+    ("pv_v3_kernel_launches", ctypes.c_int, [c_i32, c_i32, c_i32, c_i32, c_i32]),
     ("pv_ransac_voting_v3", ctypes.c_int,
      [ctypes.POINTER(ImageDesc), ctypes.POINTER(VoteParams), c_vp, c_vp, c_size, ctypes.POINTER(V3Diag), c_vp]),
     ("pv_ransac_voting_v5", ctypes.c_int,

@@ -712,6 +712,9 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_ba
 #ifndef PVC_RING4
 #define PVC_RING4 0              // 1: k_conv3x3r, 32-channel half steps in a ring of four stages (A/B: bit-identical, measured ~25 % slower)
 #endif
+#ifndef PVC_XRING3
+#define PVC_XRING3 0             // 1: k_conv3x3's pixel stages in a ring of three (issued two steps ahead), weights in two
+#endif
 #ifndef PVC_PRIO
 #define PVC_PRIO 0               // 1: s_setprio(1) around each MFMA cluster (A/B)
 #endif
@@ -831,7 +834,15 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
     constexpr int NW = (CT * RB) / (1024 * kNW);           // weight loads per wave per stage
     constexpr int WC = kNW / 4;                            // cout groups of waves
     constexpr int MI = CT / WC / 16;                       // 16-cout accumulator tiles per wave
+#if PVC_XRING3
+    // weights in a ring of two stages, pixels in a ring of three: a step's
+    // pixel loads are issued two steps ahead (their L2 / HBM latency exceeds
+    // the ~half step the two-stage form leaves them); 160 KiB at CT 256
+    constexpr int WST = CT * RB, XST = kPT * RB;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WST + 3 * XST];
+#else
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STAGE];
+#endif
     const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
     // XCD-aware tile order: blocks i, i + 8, ... share an XCD; give each XCD a
     // contiguous range of tiles, pixel tile major (PVC_PT_MAJOR)
@@ -917,13 +928,21 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
     // the K index (tap * cbk + cb: the weights' memory order) of step s
     auto kidx = [&](int s) { return s < a.nmain ? step_tap(s) * cbk + step_cb(s) : s; };
     auto issue_w = [&](int s, int buf) {
+#if PVC_XRING3
+        uint8_t *st = lds + buf * WST;
+#else
         uint8_t *st = lds + buf * STAGE;
+#endif
         const int ks = kidx(s);
 #pragma unroll
         for (int i = 0; i < NW; ++i) glds16(wr, st + (NW * wid + i) * 1024, woff[i], ks * RB);
     };
     auto issue_x = [&](int s, int buf) {
+#if PVC_XRING3
+        uint8_t *st = lds + 2 * WST + buf * XST;
+#else
         uint8_t *st = lds + buf * STAGE + CT * RB;
+#endif
         if (a.mode2 == PV_CONV_X2_1X1 && s >= a.nmain) {
             // the 1x1 second input (the BasicBlock's downsample): centre tap at stride s2
             const uint32_t cbo = (uint32_t)(s - a.nmain) * RB;
@@ -981,7 +1000,7 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
     (void)read_frags;
     (void)mfma_frags;
     // kc-th half of a step (32 of its 64 channels)
-    auto compute_kc = [&](const uint8_t *st, int kc) {
+    auto compute_kx = [&](const uint8_t *st, const uint8_t *xst, int kc) {
         {
             const int sg = kc * 4 + (lane >> 4);
             h8v af[MI], bf[4];
@@ -993,7 +1012,7 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni) {
                 const int r = wm * 64 + ni * 16 + (lane & 15);
-                bf[ni] = *(const h8v *)(st + CT * RB + conv_granule(r, sg) * 16);
+                bf[ni] = *(const h8v *)(xst + conv_granule(r, sg) * 16);
             }
 #ifdef PVC_NO_MFMA
 #pragma unroll
@@ -1013,8 +1032,29 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
 #endif
         }
     };
+    auto compute_kc = [&](const uint8_t *st, int kc) { compute_kx(st, st + CT * RB, kc); };
     const int k0 = tail < 0 ? 0 : part * ksteps / a.nsplit;
     const int k1 = tail < 0 ? ksteps : (part + 1) * ksteps / a.nsplit;
+#if PVC_XRING3
+    (void)compute_kc;
+    (void)issue;
+    issue_x(k0, 0);
+    issue_w(k0, 0);
+    if (k0 + 1 < k1) issue_x(k0 + 1, 1);
+    for (int s = k0; s < k1; ++s) {
+        const int i = s - k0, wb = i & 1, xb = i % 3;
+        // this wave's weights(s) and pixels(s) have landed: only pixels(s + 1),
+        // issued after weights(s), may still be in flight
+        if (s + 1 < k1) __builtin_amdgcn_s_waitcnt(0x0F70 | NI);
+        else __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();                              // ... every wave's; step s-1's reads are done
+        const uint8_t *wst = lds + wb * WST, *xst = lds + 2 * WST + xb * XST;
+        compute_kx(wst, xst, 0);
+        if (s + 1 < k1) issue_w(s + 1, wb ^ 1);
+        if (s + 2 < k1) issue_x(s + 2, (i + 2) % 3);
+        compute_kx(wst, xst, 1);
+    }
+#else
     issue(k0, 0);
     for (int s = k0; s < k1; ++s) {
         const int buf = (s - k0) & 1;
@@ -1056,6 +1096,7 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
             compute_kc(lds + buf * STAGE, 1);
         }
     }
+#endif
     conv_finish<CT, MI, WC>(a, acc, tail, part, n0, p0, wn, wm, lane, lds);
 }
 

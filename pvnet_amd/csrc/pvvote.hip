@@ -3802,7 +3802,7 @@ const char *pv_version(void) { return PV_VERSION; }
 const char *pv_build_config(void) {
     return "vote=k_vote_mfma(bpc=" PVV_STR(PVV_VM_BPC) ",wpe=" PVM_WPE_STR ",chunk=" PVV_STR(PVM_CHUNK) ",queue=" PVV_STR(PVM_QUEUE) ",rw=" PVV_STR(PVV_VM_RW3_0) "/"
            PVV_STR(PVV_VM_RW3_1) "/" PVV_STR(PVV_VM_RW3_2) ")"
-           " hypgen=" PVV_STR(PVV_HYPGEN)
+           " hypgen=" PVV_STR(PVV_HYPGEN) " hypfuse=" PVV_STR(PVV_HYPFUSE)
            " refine=" PVV_STR(PVV_REFINE_NJ) "x" PVV_STR(PVV_REFINE_T)
            " fg_cpb=1/" PVV_STR(8) " compact_skip=" PVV_STR(PVV_COMPACT_SKIP)
            " bytes=k_vote_bytes(rows=" PVV_STR(PVV_BYTE_HB) ",xcd=" PVV_STR(PVV_BYTES_XCD) ",bal=" PVV_STR(PVV_BYTES_BAL) ")"
@@ -4018,6 +4018,18 @@ int pv_debug_compact_trace(int on, uint64_t *host, int n) {
 size_t pv_v3_workspace_size(int32_t b, int32_t H, int32_t W, int32_t vn, int32_t n_hyp) {
     if (b <= 0 || H <= 0 || W <= 0 || vn <= 0 || n_hyp <= 0) return 0;
     return carve(nullptr, b, H, W, vn, n_hyp).total;
+}
+
+int pv_v3_kernel_launches(int32_t b, int32_t H, int32_t W, int32_t vn, int32_t n_hyp) {
+    if (b <= 0 || H <= 0 || W <= 0 || vn <= 0 || n_hyp <= 0) return 0;
+    const int64_t P = (int64_t)H * W;
+    const int nblk = (int)((P + kCompactChunk - 1) / kCompactChunk);
+    const int64_t per_img = (int64_t)vn * ((n_hyp + kGroup - 1) / kGroup) * P;
+    if (per_img >= (1ll << 31)) return 0;
+    const int chunk = (int)std::max<int64_t>(1, std::min<int64_t>(b, ((1ll << 31) - 1) / per_img));
+    const bool pre = hyp_pregen_used(vn, n_hyp);
+    const bool fuse = PVV_HYPFUSE && pre && nblk <= kHypMaxChunks;
+    return 2 + (pre && !fuse ? 1 : 0) + (b + chunk - 1) / chunk + 1;
 }
 
 int pv_ransac_voting_v3(const pv_image_desc *img, const pv_vote_params *prm, float *out, void *workspace,
