@@ -825,3 +825,56 @@ def test_random_api_votes_match_oracle(device, rv):
         rv.voting_for_hypothesis(dd, cc, hh, out, thr)
         np.testing.assert_array_equal(out.cpu().numpy(), np.where(ref == 1, 1, init), err_msg=f"case {case} OR")
         np.testing.assert_array_equal(rv.vote_counts(dd, cc, hh, thr).cpu().numpy(), ref.sum(2), err_msg=f"case {case}")
+
+
+@pytest.mark.parametrize("case", ["stress0", "stress1", "wide5000", "wide40000", "tiny17", "ragged1000"])
+def test_vote_bytes_dense_512(case, device, rv):
+    """Dense voting_for_hypothesis at hn = 512 (the bench's U1 shape, the
+    CU-balanced byte grid): every byte equals the oracle's (KU:116-125) --
+    thresholds on reference cosines and outside the
+    fast range, degenerate / huge / zero directions, hypotheses on pixel
+    centres, on the integer lattice, huge and NaN, fractional and wide-spread
+    coordinates, windows and batches cut short -- and over a byte pattern
+    left in the output (dense: every byte rewritten)."""
+    rng = np.random.default_rng(sum(map(ord, case)))
+    hn = 512
+    if case.startswith("stress"):
+        tn, vn = 3000, 2
+        coords = np.stack([rng.integers(0, 640, tn), rng.integers(0, 480, tn)], 1).astype(np.float32)
+        ang = rng.uniform(-np.pi, np.pi, (tn, vn))
+        scale = rng.choice([1.0, 1e-7, 3e-7, 0.0, 1e5, 2e19], size=(tn, vn), p=[0.9, 0.02, 0.02, 0.02, 0.02, 0.02])
+        direct = np.stack([np.cos(ang) * scale, np.sin(ang) * scale], -1).astype(np.float32)
+        hyp = np.stack([rng.uniform(-100, 700, (hn, vn)), rng.uniform(-100, 600, (hn, vn))], -1).astype(np.float32)
+        hyp[:10] = np.round(hyp[:10])
+        hyp[10:12] = coords[rng.integers(0, tn, (2, vn))]
+        hyp[12, :, 0] = 1e20
+        hyp[13] = np.nan
+        hyp[300:310] = coords[rng.integers(0, tn, (10, vn))]
+        d = hyp[20, 0] - coords[5]
+        thrs = (0.99, float(np.float32(np.dot(d, direct[5, 0]) / (np.linalg.norm(d) * np.linalg.norm(direct[5, 0])))),
+                0.0, 0.999999)
+    elif case.startswith("wide"):
+        span = float(case[4:])
+        tn, vn = 1500, 2
+        coords = (rng.random((tn, 2)) * span).astype(np.float32)
+        coords[::3] = np.round(coords[::3])
+        ang = rng.uniform(-np.pi, np.pi, (tn, vn))
+        direct = np.stack([np.cos(ang), np.sin(ang)], -1).astype(np.float32)
+        hyp = (rng.random((hn, vn, 2)) * span * 1.2 - span * 0.1).astype(np.float32)
+        thrs = (0.3, 0.9, 0.99)
+    else:
+        tn = 17 if case == "tiny17" else 1000
+        vn = 3
+        coords = np.stack([rng.integers(200, 440, tn), rng.integers(120, 360, tn)], 1).astype(np.float32)
+        kp = np.array([320.0, 240.0], np.float32)
+        d0 = kp - coords
+        ang = np.arctan2(d0[:, 1], d0[:, 0])[:, None] + rng.normal(0, 0.05, (tn, vn))
+        direct = np.stack([np.cos(ang), np.sin(ang)], -1).astype(np.float32)
+        hyp = (kp + rng.normal(0, 30, (hn, vn, 2))).astype(np.float32)
+        thrs = (0.99, 0.9)
+    for thr in thrs:
+        ref = np.zeros((hn, vn, tn), np.uint8)
+        O.voting_for_hypothesis(direct, coords, hyp, ref, thr)
+        out = torch.full(ref.shape, 5, dtype=torch.uint8, device=device)
+        rv.voting_for_hypothesis_dense(cu(direct, device), cu(coords, device), cu(hyp, device), out, thr)
+        np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"{case} thr={thr}")
