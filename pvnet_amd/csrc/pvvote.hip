@@ -234,6 +234,7 @@ struct Workspace {
     int32_t *blkcnt;    // [b][nblk]
     int32_t *grpcnt;    // [b][ceil(nblk / kFgWideCPB)]: the wide k_fg_count blocks' sums (large grids only)
     uint64_t *fgbits;   // [b][nblk][4] foreground ballot of each wave of a k_fg_count block
+    uint64_t *keptbits; // [b][nblk][4] downsampled images: k_compact's kept ballots (for compact_hyp)
     float4 *pex;        // [b][vn][P]   exact pixel data (cx, cy, nx, ny): reference operands
     float2 *hyp;        // [b][nh][vn]  (reference layout)
     float2 *hypv;       // [b][vn][nh]  keypoint-major copy (pre-generated hypotheses)
@@ -259,6 +260,7 @@ Workspace carve(void *base, int b, int H, int W, int vn, int nh) {
     w.blkcnt = (int32_t *)take(4 * b * nblk);
     w.grpcnt = (int32_t *)take(4 * b * ((nblk + 7) / 8));
     w.fgbits = (uint64_t *)take(8 * 4 * b * nblk);
+    w.keptbits = (uint64_t *)take(8 * 4 * b * nblk);
     w.pex = (float4 *)take(16 * b * vn * P);
     w.hyp = (float2 *)take(8 * (int64_t)b * nh * vn);
     w.hypv = (float2 *)take(8 * (int64_t)b * nh * vn);
@@ -446,7 +448,7 @@ __device__ __forceinline__ void compact_chunk(const VertexView &vx, int H, int W
                                               const int32_t *grpcnt, const uint64_t *fgbits, int32_t *dsagg,
                                               int nblk, int min_num, int max_num, uint64_t seed, const uint8_t *keep,
                                               int32_t *tn, int32_t *fgtot, float4 *pex, const int b, const int blk,
-                                              int *sh, int *wcnt, uint16_t *pos) {
+                                              int *sh, int *wcnt, uint16_t *pos, uint64_t *keptbits) {
     static_assert(kCompactChunk == 256, "one pixel per thread");
     const int64_t P = (int64_t)H * W;
     const int wid = threadIdx.x / 64, lane = lane_id();
@@ -495,6 +497,12 @@ __device__ __forceinline__ void compact_chunk(const VertexView &vx, int H, int W
     const uint64_t bal = ds ? ballot(f) : fw;
     const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
     if (lane == 0) wcnt[wid] = __popcll(bal);
+    if (ds && keptbits && lane == 0) {
+        // the kept ballots for compact_hyp, stored before this block's
+        // look-back value is published (the barrier below orders them)
+        st_agent(&keptbits[((int64_t)b * nblk + blk) * 4 + wid], bal);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     // this pixel's vertex loads (all keypoints of a group in flight together),
     // issued before the block's offsets are known: buffer loads through a
     // per-image descriptor, one VGPR offset for the pixel and the keypoint /
@@ -652,6 +660,7 @@ struct HypGen {
     float2 *hyp_out;            // [b][nh][vn]
     float2 *hypv_out;           // [b][vn][nh]
     float *diag_hyp;            // [b][nh][vn][2] or nullptr
+    uint64_t *keptbits;         // downsampled images: the compaction blocks' kept ballots [b][nblk][4]
 };
 
 template <int VK>
@@ -735,6 +744,7 @@ __device__ void compact_hyp(const VertexView &vx, int H, int W, int nblk, const 
         return g.keep ? g.keep[b * P + p] != 0 : rand_unit(g.kseed, (uint64_t)b * P + p) < pk;
     };
     int n = fgb;
+    uint32_t seen = 0;                             // ds: chunks whose kept count (and ballots) were published
     if (ds) {
         // kept counts from the compaction blocks' look-back values (count + 1)
         const uint64_t t_dead = __builtin_amdgcn_s_memrealtime() + kLookbackSpin;
@@ -747,6 +757,7 @@ __device__ void compact_hyp(const VertexView &vx, int H, int W, int nblk, const 
                 __builtin_amdgcn_s_sleep(1);
                 v = ld_agent(&dsagg[b * nblk + j]);
             }
+            if (v != 0) seen |= 1u << k;
             if (v == 0) {                          // worked out from the ballots and keep decisions
                 for (int q = 0; q < 4; ++q) {
                     uint64_t w = fgbits[((int64_t)b * nblk + j) * 4 + q];
@@ -760,6 +771,15 @@ __device__ void compact_hyp(const VertexView &vx, int H, int W, int nblk, const 
             c[k] = v - 1;
         }
         n = scan(c);
+        // which chunks' kept ballots are published: bit j of the LDS words
+        // after pre[] (pre[nblk + 1 ...]); the rest are worked out below
+        int32_t *pub = pre + nblk + 1;
+        for (int q = (int)threadIdx.x; q < (nblk + 31) / 32; q += 256) pub[q] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            if ((seen >> k) & 1u) atomicOr(&pub[(j0 + k) >> 5], 1 << ((j0 + k) & 31));
+        __syncthreads();
     }
     n = min(n, (int)P);
     if (n <= 0) return;
@@ -795,9 +815,21 @@ __device__ void compact_hyp(const VertexView &vx, int H, int W, int nblk, const 
         w1[q] = fgbits[((int64_t)b * nblk + jj[1]) * 4 + q];
     }
     if (ds) {                                      // keep only the kept pixels' bits
+        const int32_t *pub = pre + nblk + 1;
+        const bool p0 = g.keptbits && ((pub[jj[0] >> 5] >> (jj[0] & 31)) & 1);
+        const bool p1 = g.keptbits && ((pub[jj[1] >> 5] >> (jj[1] & 31)) & 1);
+        // published: the compaction block's own kept ballots (one load)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            uint64_t m0 = 0, m1 = 0, x0 = w0[q], x1 = w1[q];
+            if (p0) w0[q] = ld_agent(&g.keptbits[((int64_t)b * nblk + jj[0]) * 4 + q]);
+            if (p1) w1[q] = ld_agent(&g.keptbits[((int64_t)b * nblk + jj[1]) * 4 + q]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (p0 && p1) break;
+            uint64_t m0 = w0[q], m1 = w1[q], x0 = p0 ? 0 : w0[q], x1 = p1 ? 0 : w1[q];
+            if (!p0) m0 = 0;
+            if (!p1) m1 = 0;
             while (x0) { const int z = __builtin_ctzll(x0); x0 &= x0 - 1;
                          if (kept((int64_t)jj[0] * kCompactChunk + q * 64 + z)) m0 |= 1ull << z; }
             while (x1) { const int z = __builtin_ctzll(x1); x1 &= x1 - 1;
@@ -840,13 +872,14 @@ __global__ __launch_bounds__(256) void k_compact(MaskView, VertexView vx, int H,
     __shared__ int sh[8];
     __shared__ int wcnt[4];
     __shared__ uint16_t pos[TASKS ? kCompactChunk : 1];
-    __shared__ int32_t pre[kHypMaxChunks + 1];
+    __shared__ int32_t pre[kHypMaxChunks + 1 + (kHypMaxChunks + 31) / 32];
     if ((int)blockIdx.x < g.nhb) {
         compact_hyp<KIND, EVD, VK>(vx, H, W, nblk, blkcnt, fgbits, dsagg, pre, sh, g, (int)blockIdx.y, (int)blockIdx.x);
         return;
     }
     compact_chunk<KIND, EVD, VK, TASKS>(vx, H, W, vn, blkcnt, grpcnt, fgbits, dsagg, nblk, min_num, max_num, seed, keep, tn,
-                                        fgtot, pex, (int)blockIdx.y, (int)blockIdx.x - g.nhb, sh, wcnt, pos);
+                                        fgtot, pex, (int)blockIdx.y, (int)blockIdx.x - g.nhb, sh, wcnt, pos,
+                                        g.nhb > 0 ? g.keptbits : nullptr);
 }
 
 // ==========================================================================
@@ -3727,6 +3760,7 @@ int front_half(const pv_image_desc *img, const pv_vote_params *prm, int nh, bool
         ca.hg.seed = mix64(prm->seed); ca.hg.kseed = ca.seed;
         ca.hg.idxs = prm->idxs; ca.hg.keep = prm->keep;
         ca.hg.hyp_out = w.hyp; ca.hg.hypv_out = w.hypv; ca.hg.diag_hyp = dg.hyp;
+        ca.hg.keptbits = w.keptbits;
     }
     int r = dispatch_mask<CompactStage>(img->mask_kind, evd, (const CompactArgs *)&ca);
     if (r) return r;
