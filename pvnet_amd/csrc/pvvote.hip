@@ -1705,7 +1705,13 @@ __device__ __forceinline__ uint4 form_row(float ax, float ay, float b) {
 #define PVM_ALIGNED 0
 #endif
 #ifndef PVM_WPE
-#define PVM_WPE 3   // 152 VGPRs, no spills (4: 128, spilled across the hot loop): 40.4k -> 41.5k images/s
+// waves per SIMD the registers are sized for.  Round 2: 3 (152 VGPRs; 4 then
+// spilled across the hot loop): 40.4k -> 41.5k images/s.  Round 6: the kernel
+// needs 129 at 3 -- one over the 128 that lets a fourth wave, the next
+// frame's block, share the SIMD -- and fits 122 without spills at 4: the
+// batch-1 stream 53.2-53.5k -> 54.2-54.6k images/s, latency unchanged
+// (profiles/r06/vote_wpe_ab.txt)
+#define PVM_WPE 4
 #endif
 #define PVM_WPE_STR2(x) #x
 #define PVM_WPE_STR3(x) PVM_WPE_STR2(x)
