@@ -46,9 +46,9 @@ FP32_VECTOR_PEAK_TFLOPS = 157.3
 H, W, VN = 480, 640, 9
 
 
-PMC_FILE = "profiles/r05_pmc_traffic.json"
+PMC_FILE = "profiles/r06_pmc_traffic.json"
 U1_WARM, U1_TIMED = 5, 3            # measure_u1: graph replays (of 100 launches) untimed, then timed
-STATS_FILE = "profiles/r05_bench_kernel_stats.csv"
+STATS_FILE = "profiles/r06_bench_kernel_stats.csv"
 
 
 def pmc_traffic(kernel):
