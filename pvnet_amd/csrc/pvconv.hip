@@ -55,6 +55,9 @@
 #ifndef PVC_L1_AHEAD
 #define PVC_L1_AHEAD 2      // halo kernels (k_conv64, k_dec_conv2s / 4s): fragment reads this many k-steps ahead of their MFMAs
 #endif
+#ifndef PVC_DEC_BAL
+#define PVC_DEC_BAL 0       // conv2s (k_dec_conv<32, 2>): three halo buffers, each blend spread over two phases (0: one phase each)
+#endif
 
 namespace {
 
@@ -104,6 +107,23 @@ struct TailArgs {
 #else
 #define PVT_STAMP(k)
 #endif
+
+#ifndef PVC_XCD_TILES
+#define PVC_XCD_TILES 1     // persistent halo kernels: each XCD takes a contiguous range of a round's tiles (0: block-cyclic)
+#endif
+// Blocks b, b + 8, ... run on one XCD (the dispatcher deals blocks round
+// robin over the 8 XCDs).  Renumbered so that XCD x holds a contiguous range
+// of [0, nb): in a round of a persistent grid its blocks take neighbouring
+// tiles, whose shared halo rows and columns then meet in that XCD's L2.
+__device__ __forceinline__ int xcd_block(int bid, int nb) {
+#if PVC_XCD_TILES
+    const int q = nb / 8, r = nb % 8, x = bid % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+#else
+    (void)nb;
+    return bid;
+#endif
+}
 
 __device__ __forceinline__ void tile_coords(const TailArgs &a, int tile, int &b, int &y0, int &x0, int &ly0,
                                             int &lx0) {
@@ -330,17 +350,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVT_WPE, PV
         bias[i] = i < 32 ? (_Float16)a.b1[i] : (i - 32 < COUT ? (_Float16)a.b2[i - 32] : (_Float16)0.f);
     const Geo g = make_geo((int)threadIdx.x);
     // the next tile's inputs are fetched during this tile's convolution
-    int tile = (int)blockIdx.x;
+    int tile = xcd_block((int)blockIdx.x, (int)gridDim.x);
     if (tile < a.ntiles) fetch(a, tile, patch, imgs);
+    __builtin_amdgcn_s_waitcnt(0x0F70);                // the first tile's inputs have landed
     for (int it = 0; tile < a.ntiles; tile += (int)gridDim.x, ++it) {
         (void)it;
         PVT_STAMP(0);
         int b, y0, x0, ly0, lx0;
         tile_coords(a, tile, b, y0, x0, ly0, lx0);
-        // this wave's patch / image loads have landed (vmcnt 0: its last tile's
-        // stores are out too), then every wave's; every wave is also past the
-        // previous tile's convolution (halo reads)
-        __builtin_amdgcn_s_waitcnt(0x0F70);
+        // this wave's patch / image loads landed before its last epilogue
+        // (whose stores may still be in flight); the barrier: every wave's,
+        // and every wave is past the previous tile's convolution (halo reads)
         PVT_STAMP(1);
         __syncthreads();
         PVT_STAMP(2);
@@ -401,6 +421,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVT_WPE, PV
 #else
         acc[0][0] = (float)halo[threadIdx.x];
 #endif
+        // the next tile's fetch (issued before the convolution) has landed, and
+        // the previous tile's stores are out; this tile's stay in flight
+        __builtin_amdgcn_s_waitcnt(0x0F70);
         PVT_STAMP(7);
         // ---- epilogue + head, per row ----
         const TailOut to = tail_out<COUT>(a, b);
@@ -1561,8 +1584,9 @@ __global__ __launch_bounds__(512) void k_dec_conv2s(DecConvArgs a) {
         }
     };
     __builtin_amdgcn_s_waitcnt(0x0F70);
-    int tile = (int)blockIdx.x;
+    int tile = xcd_block((int)blockIdx.x, (int)gridDim.x);
     if (tile < a.ntiles) fetch(tile);
+    __builtin_amdgcn_s_waitcnt(0x0F70);                // (every tile starts with its halo registers landed)
     for (; tile < a.ntiles; tile += (int)gridDim.x) {
         int b, y0, x0, ly0, lx0;
         coords(tile, b, y0, x0, ly0, lx0);
@@ -1932,10 +1956,27 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_conv(DecConvArgs a) {
     // this tile's are consumed): one register set each
     constexpr int LP = NUP == 2 ? 0 : 2, LS = P - 1, SS = 1;
     static_assert(P % 2 == 0 && PIECES * 1024 == WB, "part parity and whole DMA pieces");
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WB + 2 * kXHaloB + 2 * kXPatchB];
-    uint8_t *const wbuf = lds, *const hbuf = lds + 2 * WB, *const pbuf = lds + 2 * WB + 2 * kXHaloB;
+    // BAL (conv2s): parts in the order up0, skip0, up1, skip1, each in halo
+    // buffer (part count) mod 3, so that part k can be built over phases k - 2
+    // and k - 1: an upsampled part's blend is split in two halves, one per
+    // phase, and every phase's producer work is half a blend (+ a skip copy in
+    // phases 0 and 2) instead of a whole blend in two phases of four and a
+    // copy in the other two (the blend phases were producer-bound, the copy
+    // phases consumer-bound).
+    constexpr bool BAL = PVC_DEC_BAL && NUP == 2;
+    constexpr int NH = BAL ? 3 : 2;                    // halo buffers
+    // the weight part (32-channel block of cat([up(fm), skip])) of phase j
+    auto wpart = [](int j) { return BAL ? ((j >> 1) | ((j & 1) << 1)) : j; };
+    // store instructions of a tile's epilogue (every one issued, out-of-range
+    // pixels' dropped by the buffer range): the last phase's wait leaves them
+    // in flight and waits for the weight DMA issued before them
+    constexpr int NST = kDecRows * MT * 4;
+    static_assert(NST <= 15, "vmcnt immediate");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WB + NH * kXHaloB + 2 * kXPatchB + CO * 2];
+    uint8_t *const wbuf = lds, *const hbuf = lds + 2 * WB, *const pbuf = lds + 2 * WB + NH * kXHaloB;
+    _Float16 *const bl = (_Float16 *)(lds + 2 * WB + NH * kXHaloB + 2 * kXPatchB);   // the bias (consumers)
     const int t = (int)threadIdx.x, lane = t & 63, wid = t >> 6;
-    const int n = lane & 31, h = lane >> 5;
+    [[maybe_unused]] const int n = lane & 31, h = lane >> 5;
     const bool consumer = wid < kDecCW;
     const int pt = t - kDecCW * 64;                    // producer thread (0..511)
     const int G = (int)gridDim.x;
@@ -1950,8 +1991,8 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_conv(DecConvArgs a) {
     // ---- consumers: weights by LDS-DMA, MFMAs, epilogue ----
     const __amdgpu_buffer_rsrc_t wr =
         __builtin_amdgcn_make_buffer_rsrc((void *)a.w, 0, (P / 2) * 9 * 8 * CO * 16, 0x00020000);
-    auto dma_weights = [&](int part) {                 // consumer waves: pieces wid, wid + kDecCW, ...
-        uint8_t *dst = wbuf + (part & 1) * WB;
+    auto dma_weights = [&](int part, int buf) {        // consumer waves: pieces wid, wid + kDecCW, ...
+        uint8_t *dst = wbuf + buf * WB;
         const int p64 = part >> 1, q0 = (part & 1) * 4;
         for (int i = wid; i < PIECES; i += kDecCW) {
             const int byte = i * 1024 + lane * 16;
@@ -1964,8 +2005,8 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_conv(DecConvArgs a) {
     // k-step s (tap s >> 1, channel half s & 1 of the part): the weight
     // fragments once, the halo fragment of each of the wave's rows; the
     // summation order of every output is the one-row form's
-    auto mfma_part = [&](int part) {
-        const uint8_t *W = wbuf + (part & 1) * WB, *Hb = hbuf + (part & 1) * kXHaloB;
+    auto mfma_part = [&](int wb, int hb) {
+        const uint8_t *W = wbuf + wb * WB, *Hb = hbuf + hb * kXHaloB;
         auto frag = [&](int s, h8 (&bf)[kDecRows], h8 (&af)[MT]) {
             const int o = 2 * s + h, tap = o >> 2, q = o & 3;
             const int ky = tap / 3, kx = tap - 3 * ky;
@@ -1994,11 +2035,12 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_conv(DecConvArgs a) {
     auto epilogue = [&](int tile) {
         int b, y0, x0, ly0, lx0;
         coords(tile, b, y0, x0, ly0, lx0);
+        const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(a.out + (int64_t)b * a.H * a.W * CO), 0, a.H * a.W * CO * 2, 0x00020000);
 #pragma unroll
         for (int r = 0; r < kDecRows; ++r) {
-        const int oy = y0 + kDecRows * wid + r, ox = x0 + n;
-        if (oy < a.H && ox < a.W) {
-            _Float16 *op = a.out + (((int64_t)b * a.H + oy) * a.W + ox) * CO;
+            const int oy = y0 + kDecRows * wid + r, ox = x0 + n;
+            const uint32_t po = oy < a.H && ox < a.W ? (uint32_t)((oy * a.W + ox) * CO * 2) : 0x80000000u;
 #pragma unroll
             for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -2006,13 +2048,13 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_conv(DecConvArgs a) {
                     h4 y;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) y[j] = (_Float16)acc[r][m][4 * g + j];
-                    y = y + *(const h4 *)(a.bias + 32 * m + 8 * g + 4 * h);   // (cached; not held in registers)
+                    y = y + *(const h4 *)(bl + 32 * m + 8 * g + 4 * h);
                     h4 ys;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) ys[j] = (_Float16)((float)y[j] * a.slope);
-                    *(h4 *)(op + 32 * m + 8 * g + 4 * h) = __builtin_elementwise_max(y, ys);
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, __builtin_elementwise_max(y, ys)), orr,
+                                                          po + (32 * m + 8 * g + 4 * h) * 2, 0, 0);
                 }
-        }
         }
     };
     // ---- producers: loads into registers, patch writes, halo builds ----
@@ -2058,8 +2100,8 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_conv(DecConvArgs a) {
         for (int i = 0; i < kXPatchIt; ++i)
             if (pt + 512 * i < kXPatch) *(h8 *)(pb + (pt + 512 * i) * 16) = preg[up & 1][i];
     };
-    auto build_skip = [&](int sp, int part, const h8 (&sr)[2][kXSkipIt]) {
-        uint8_t *hb = hbuf + (part & 1) * kXHaloB;
+    auto build_skip = [&](int sp, int hidx, const h8 (&sr)[2][kXSkipIt]) {
+        uint8_t *hb = hbuf + hidx * kXHaloB;
 #pragma unroll
         for (int i = 0; i < kXSkipIt; ++i) {
             const int c = pt + 512 * i;
@@ -2125,13 +2167,15 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_conv(DecConvArgs a) {
         tasks(std::integral_constant<int, 2>{}, std::integral_constant<int, 3>{});
     };
 
-    int tile = (int)blockIdx.x;
+    int tile = xcd_block((int)blockIdx.x, G);
     if (tile >= a.ntiles) return;
     // The two roles run separate loops (so that their registers -- the
     // accumulators and fragments, the prefetched inputs -- share the file)
     // with the same barriers: two in the prologue, one per phase.
     if (consumer) {
-        dma_weights(0);                                // part 0's weights
+        if (wid == 0 && lane < CO / 4) *(h4 *)(bl + 4 * lane) = *(const h4 *)(a.bias + 4 * lane);
+        dma_weights(wpart(0), 0);                      // phase 0's weights
+        int hk = 0;                                    // this phase's halo buffer
         __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0)
         __syncthreads();
         __syncthreads();
@@ -2145,15 +2189,149 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_conv(DecConvArgs a) {
 #pragma unroll 1     // (unrolled, the phases' fragment and DMA registers overlap: spills at MT = 2)
             for (int j = 0; j < P; ++j) {
                 PVD_STAMP(it, j, 0);
-                if (j + 1 < P || more) dma_weights((j + 1) % P);
-                mfma_part(j);
-                if (j == P - 1) epilogue(tile);
+                if (j + 1 < P || more) dma_weights(wpart((j + 1) % P), (j + 1) & 1);
+                mfma_part(j & 1, BAL ? hk : (j & 1));
+                hk = hk == NH - 1 ? 0 : hk + 1;
                 PVD_STAMP(it, j, 1);
-                __builtin_amdgcn_s_waitcnt(0x0F70);    // this wave's weight pieces (and stores) have landed
+                // this wave's weight pieces have landed, then every wave's (and
+                // every wave's fragment reads of this part are done).  A plain
+                // barrier: through __syncthreads' fence the compiler waits for
+                // the epilogue's stores too (vmcnt(0)), ~4k cycles a tile
+                if (j == P - 1) {
+                    epilogue(tile);
+                    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NST) : "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                }
                 PVD_STAMP(it, j, 2);
-                __syncthreads();
             }
             tile += G;
+            if (!more) break;
+        }
+        return;
+    }
+    if constexpr (BAL) {
+        // one skip part's halo chunks into sreg[0][u] (a tile past the last reads nothing)
+        auto load_skip1 = [&](int tile, int u) {
+            int b, y0, x0, ly0, lx0;
+            coords(min(tile, a.ntiles - 1), b, y0, x0, ly0, lx0);
+            const __amdgpu_buffer_rsrc_t sr_ = __builtin_amdgcn_make_buffer_rsrc(
+                (void *)(a.skip + (int64_t)b * a.H * a.W * 64), 0, a.H * a.W * 64 * 2, 0x00020000);
+#pragma unroll
+            for (int i = 0; i < kXSkipIt; ++i) {
+                const int c = min(pt + 512 * i, kXHalo - 1), hp = c >> 2, q = c & 3;
+                const int hy = hp / kHC, hx = hp - hy * kHC;
+                const int oy = y0 - 1 + hy, ox = x0 - 1 + hx;
+                const bool ok = tile < a.ntiles && oy >= 0 && oy < a.H && ox >= 0 && ox < a.W;
+                const uint32_t off = ok ? (uint32_t)((oy * a.W + ox) * 128 + q * 16) : 0x80000000u;
+                sreg[0][u][i] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(sr_, off, u * 64, 0));
+            }
+        };
+        // half hf of an upsampled part's blend (halo chunks [680 hf, 680 hf + 680):
+        // this thread's pt + 680 hf and, for pt < 168, + 512) from patch slot
+        // `slot` into halo buffer hidx; the same arithmetic as build_up
+        auto build_half = [&](int tile, int slot, int hidx, int hf) {
+            int b, y0, x0, ly0, lx0;
+            coords(tile, b, y0, x0, ly0, lx0);
+            const uint8_t *pb = pbuf + slot * kXPatchB;
+            uint8_t *hb = hbuf + hidx * kXHaloB;
+            const int q = pt & 3;
+            constexpr int kHalf = kXHalo / 2;
+            static_assert(kHalf % 4 == 0 && kHalf > 512 && kHalf <= 1024, "two tasks per thread and half");
+            const int cs[2] = {kHalf * hf + pt, kHalf * hf + pt + 512};
+            h8 A[2], B[2], C[2], D[2];
+            float wl[2], hl[2];
+            bool in[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int hp = min(cs[k], kXHalo - 1) >> 2, hy = hp / kHC, hx = hp - hy * kHC;
+                const int oy = y0 - 1 + hy, ox = x0 - 1 + hx;
+                in[k] = oy >= 0 && oy < a.H && ox >= 0 && ox < a.W;
+                const int oyc = min(max(oy, 0), a.H - 1), oxc = min(max(ox, 0), a.W - 1);
+                const float w1r = a.rw * (float)oxc, h1r = a.rh * (float)oyc;
+                const int w1 = (int)w1r, h1 = (int)h1r;
+                const int dw = w1 < a.Win - 1 ? 4 : 0, dh = h1 < a.Hin - 1 ? kPC * 4 : 0;
+                wl[k] = w1r - (float)w1;
+                hl[k] = h1r - (float)h1;
+                const uint8_t *pp = pb + (((h1 - ly0) * kPC + (w1 - lx0)) * 4 + q) * 16;
+                A[k] = *(const h8 *)pp;
+                B[k] = *(const h8 *)(pp + dw * 16);
+                C[k] = *(const h8 *)(pp + dh * 16);
+                D[k] = *(const h8 *)(pp + (dh + dw) * 16);
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                if (k == 1 && pt + 512 >= kHalf) break;
+                const h8 ww = (h8)(_Float16)wl[k], w0 = (h8)(_Float16)(1.f - wl[k]);
+                const h8 c0 = __builtin_elementwise_fma(B[k], ww, A[k] * w0);
+                const h8 c1 = __builtin_elementwise_fma(D[k], ww, C[k] * w0);
+                h8 v = __builtin_elementwise_fma(c1, (h8)(_Float16)hl[k], c0 * (h8)(_Float16)(1.f - hl[k]));
+                if (!in[k]) v = h8{};
+                *(h8 *)(hb + halo32(cs[k] >> 2, q) * 16) = v;
+            }
+        };
+        auto hnext = [](int h, int d) { h += d; return h >= 3 ? h - 3 : h; };
+        // prologue: tile 0's patches (slots 0, 1) and skip parts; up0 built
+        // whole into halo buffer 0 (phase 0's); up0 of the next tile loading
+        load_patch(tile, 0, 2);
+        load_skip1(tile, 0);
+        load_skip1(tile, 1);
+        write_patch(0);
+        write_patch(1);
+        __syncthreads();
+        build_half(tile, 0, 0, 0);
+        build_half(tile, 0, 0, 1);
+        load_patch(tile + G, 0, 1);
+        __syncthreads();
+        // phase j: the consumers read halo buffer hk; this phase finishes part
+        // k + 1 (buffer hk + 1) and starts part k + 2 (hk + 2), mod 3
+        int hk = 0;
+        [[maybe_unused]] int it = 0;                   // (trace builds: the tile iteration)
+        for (;;) {
+            const int nxt = tile + G;
+            const bool more = nxt < a.ntiles;
+            // phase 0: skip0 copied, up1's first half; slot 0 <- up0(nxt); loads up1(nxt)
+            PVD_STAMP(it, 0, 4);
+            build_skip(0, hnext(hk, 1), sreg[0]);
+            build_half(tile, 1, hnext(hk, 2), 0);
+            PVD_STAMP(it, 0, 5);
+            write_patch(0);
+            PVD_STAMP(it, 0, 6);
+            load_patch(nxt, 1, 2);
+            PVD_STAMP(it, 0, 7);
+            __syncthreads();
+            hk = hnext(hk, 1);
+            // phase 1: up1's second half; loads skip0(nxt), up0(nxt + G)
+            PVD_STAMP(it, 1, 4);
+            build_half(tile, 1, hnext(hk, 1), 1);
+            PVD_STAMP(it, 1, 5);
+            PVD_STAMP(it, 1, 6);
+            load_skip1(nxt, 0);
+            load_patch(nxt + G, 0, 1);
+            PVD_STAMP(it, 1, 7);
+            __syncthreads();
+            hk = hnext(hk, 1);
+            // phase 2: skip1 copied, up0(nxt)'s first half; slot 1 <- up1(nxt)
+            PVD_STAMP(it, 2, 4);
+            build_skip(1, hnext(hk, 1), sreg[0]);
+            if (more) build_half(nxt, 0, hnext(hk, 2), 0);
+            PVD_STAMP(it, 2, 5);
+            write_patch(1);
+            PVD_STAMP(it, 2, 6);
+            PVD_STAMP(it, 2, 7);
+            __syncthreads();
+            hk = hnext(hk, 1);
+            // phase 3: up0(nxt)'s second half; loads skip1(nxt)
+            PVD_STAMP(it, 3, 4);
+            if (more) build_half(nxt, 0, hnext(hk, 1), 1);
+            PVD_STAMP(it, 3, 5);
+            PVD_STAMP(it, 3, 6);
+            load_skip1(nxt, 1);
+            PVD_STAMP(it, 3, 7);
+            __syncthreads();
+            hk = hnext(hk, 1);
+            tile = nxt;
+            ++it;
             if (!more) break;
         }
         return;
@@ -2180,7 +2358,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_conv(DecConvArgs a) {
             PVD_STAMP(it, j, 4);
             const int m = j + 1;                       // the part this phase builds
             if (m < NUP) build_up(tile, m);
-            else if (m < P) build_skip(m - NUP, m, sreg[S]);
+            else if (m < P) build_skip(m - NUP, m & 1, sreg[S]);
             else if (more) build_up(nxt, 0);
             PVD_STAMP(it, j, 5);
             // patches two phases ahead of their builds
@@ -2266,8 +2444,9 @@ __global__ __launch_bounds__(512) void k_conv64(L1Args a) {
         }
     };
     __builtin_amdgcn_s_waitcnt(0x0F70);
-    int tile = (int)blockIdx.x;
+    int tile = xcd_block((int)blockIdx.x, (int)gridDim.x);
     if (tile < a.ntiles) fetch(tile);
+    __builtin_amdgcn_s_waitcnt(0x0F70);                // (every tile starts with its halo registers landed)
     for (; tile < a.ntiles; tile += (int)gridDim.x) {
         int b, y0, x0;
         coords(tile, b, y0, x0);
@@ -2314,6 +2493,10 @@ __global__ __launch_bounds__(512) void k_conv64(L1Args a) {
             acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f0[c], fb[c], acc[0], 0, 0, 0);
             acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f1[c], fb[c], acc[1], 0, 0, 0);
         }
+        // the next tile's halo registers and the residual have landed (and the
+        // previous tile's stores are out): the stores below stay in flight
+        // through the next tile's halo write instead of being waited for there
+        __builtin_amdgcn_s_waitcnt(0x0F70);
         // ---- epilogue: acc[m] rows (i & 3) + 8 (i >> 2) + 4 h = couts 32 m + .., column n = pixel ----
         if (pix_ok) {
 #pragma unroll

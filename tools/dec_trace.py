@@ -49,10 +49,11 @@ for name, C1, CO, h, w in (("conv4s", 128, 64, 60, 80), ("conv2s", 64, 32, 120, 
         d_wait = (t[:, 1:, j, 2] - t[:, 1:, j, 1])[sel]
         nxt = np.where(j + 1 < P, t[:, 1:, min(j + 1, P - 1), 0], np.roll(t[:, :, 0, 0], -1, axis=1)[:, 1:])
         d_phase = (nxt - t[:, 1:, j, 0])[sel & (nxt > 0)]
-        p_load = (t[:, 1:, j, 5] - t[:, 1:, j, 4])[sel]
-        p_build = (t[:, 1:, j, 6] - t[:, 1:, j, 5])[sel]
-        p_write = (t[:, 1:, j, 7] - t[:, 1:, j, 6])[sel]
+        # producer stamps: [4] phase start, [5] build done, [6] patch writes done, [7] loads issued
+        p_build = (t[:, 1:, j, 5] - t[:, 1:, j, 4])[sel]
+        p_write = (t[:, 1:, j, 6] - t[:, 1:, j, 5])[sel]
+        p_load = (t[:, 1:, j, 7] - t[:, 1:, j, 6])[sel]
         p_arrive = (t[:, 1:, j, 7] - t[:, 1:, j, 0])[sel]
         print(f"  phase {j}: phase {np.median(d_phase):7.0f}  cons mfma {np.median(d_mfma):6.0f} wait {np.median(d_wait):6.0f}"
-              f" | prod loads {np.median(p_load):6.0f} build {np.median(p_build):6.0f} writes {np.median(p_write):6.0f}"
+              f" | prod build {np.median(p_build):6.0f} patch writes {np.median(p_write):6.0f} loads {np.median(p_load):6.0f}"
               f" done@ {np.median(p_arrive):6.0f}", flush=True)
