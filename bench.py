@@ -1316,7 +1316,9 @@ def report(args, ws, res, final_err, dev):
               note="algorithmic bytes H*W*(2+2K)*4 + tn*(2K+2)*4 (SURVEY 8(d) U3) / the two kernels' time "
                    "between an event recorded before the call and the library's ev_compact_end, eager calls "
                    "(launch gaps included); the pipeline writes 16 B per pixel and keypoint (the reference's "
-                   "(cx, cy, nx, ny) operands), not 8; traffic = the two kernels' PMC bytes (%s)" % PMC_FILE)
+                   "(cx, cy, nx, ny) operands), not 8; since round 6 the k_compact launch also makes the "
+                   "frame's hypotheses (its first blocks, PVV_HYPFUSE), so this time includes that work (U2's "
+                   "input, not U3's bytes); traffic = the two kernels' PMC bytes (%s)" % PMC_FILE)
     line = {
         "metric": "images/sec (480x640, 9 kp) vote->keypoint",
         "value": round(value, 2),
