@@ -847,8 +847,17 @@ __device__ __forceinline__ void conv_finish(const ConvArgs &a, f4v (&acc)[MI][4]
     }
 }
 
+#ifdef PVC_CLOCK_TRACE
+// diagnostic builds only: per block, s_memtime and s_memrealtime (100 MHz)
+// before the K loop and after it -- the in-kernel shader clock (MI355X_MICROARCH
+// "DVFS give-back": MFMA-dense loops hold the clock well below 2.4 GHz)
+__device__ unsigned long long *g_conv_clk;
+#endif
 template <int CT>
 __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
+#ifdef PVC_CLOCK_TRACE
+    const unsigned long long ck0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     constexpr int KB = 64;                                 // K-step: one tap x 64 input channels
     constexpr int RB = KB * 2;                             // bytes per LDS row
     constexpr int STAGE = (CT + kPT) * RB;                 // 64 KiB (CT 256), 48 KiB (CT 128)
@@ -1118,6 +1127,12 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
             compute_kc(lds + buf * STAGE, 0);
             compute_kc(lds + buf * STAGE, 1);
         }
+    }
+#endif
+#ifdef PVC_CLOCK_TRACE
+    if (g_conv_clk && threadIdx.x == 0 && tail < 0) {
+        unsigned long long *q = g_conv_clk + (int64_t)blockIdx.x * 4;
+        q[0] = ck0; q[1] = rt0; q[2] = __builtin_amdgcn_s_memtime(); q[3] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
     conv_finish<CT, MI, WC>(a, acc, tail, part, n0, p0, wn, wm, lane, lds);
@@ -2754,6 +2769,11 @@ extern "C" int pv_decoder_conv2s_f16(const void *fm, const void *skip, const voi
     return e == hipSuccess ? PV_OK : (int)e;
 }
 
+#ifdef PVC_CLOCK_TRACE
+extern "C" int pv_debug_set_conv_clk(void *p) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_conv_clk), &p, sizeof(p));
+}
+#endif
 #ifdef PVC_DEC_TRACE
 extern "C" int pv_debug_set_dec_trace(void *p) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_dec_trace), &p, sizeof(p));
