@@ -744,6 +744,18 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_ba
 #ifndef PVC_ISSUE_MID
 #define PVC_ISSUE_MID 2          // 0 before the step's MFMAs, 1 after its first half, 2 = 1 for 256-cout tiles only
 #endif
+#ifndef PVC_REGSTAGE
+// 1: k_conv3x3's operands staged through registers (buffer_load to VGPRs,
+// ds_write_b128 into the stage) instead of buffer loads to LDS.  A step's
+// loads are issued two steps ahead and written into the free stage in the
+// middle of the step before their use, so each load has a whole step
+// (~3k cycles) to arrive.  The LDS-DMA form cannot keep loads in flight
+// across a barrier: the compiler waits for every outstanding LDS-DMA
+// (vmcnt(0)) before the next ds_read of the LDS it may alias -- which also
+// drained PVC_XRING3's third stage at every step.  Measured 7-9 % slower on
+// every wide shape (profiles/r06/conv_regstage_ab.txt); kept off.
+#define PVC_REGSTAGE 0
+#endif
 constexpr int kNW = PVC_NW;                   // waves per block: 16 (4 cout x 4 pixel groups; 8 = 2 x 4 measured 5-8 % slower)
 
 // The end of a k_conv3x3 / k_conv3x3w tile: a split tile's part hands its
@@ -1067,7 +1079,55 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
     auto compute_kc = [&](const uint8_t *st, int kc) { compute_kx(st, st + CT * RB, kc); };
     const int k0 = tail < 0 ? 0 : part * ksteps / a.nsplit;
     const int k1 = tail < 0 ? ksteps : (part + 1) * ksteps / a.nsplit;
-#if PVC_XRING3
+#if PVC_REGSTAGE && !PVC_XRING3
+    (void)issue;
+    // the same source offsets and LDS image as issue_w / issue_x (granule g of
+    // the stage <- the lane's swizzled 16-byte source segment), by way of
+    // registers: rw / rx hold step s + 1's operands while step s computes
+    u4 rw[NW], rx[NI];
+    auto load_regs = [&](int s) {
+        const int ks = kidx(s);
+#pragma unroll
+        for (int i = 0; i < NW; ++i) rw[i] = __builtin_amdgcn_raw_buffer_load_b128(wr, woff[i], ks * RB, 0);
+        if (a.mode2 == PV_CONV_X2_1X1 && s >= a.nmain) {
+            const uint32_t cbo = (uint32_t)(s - a.nmain) * RB;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) rx[i] = __builtin_amdgcn_raw_buffer_load_b128(x2r, pb2[i] + cbo, 0, 0);
+            return;
+        }
+        const int tap = step_tap(s), cb = step_cb(s);
+        const int dy = (tap / 3 - 1) * a.dil, dx = (tap % 3 - 1) * a.dil;
+        const bool second = a.mode2 == PV_CONV_X2_CAT && cb >= a.cb1;
+        const int C = second ? a.Cin2 : a.Cin, cbo = (second ? cb - a.cb1 : cb) * RB;
+        const uint32_t delta = (uint32_t)((dy * a.Win + dx) * C * 2 + cbo);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const bool ok = (unsigned)(pyb[i] + dy) < (unsigned)a.Hin && (unsigned)(pxb[i] + dx) < (unsigned)a.Win;
+            const uint32_t off = ok ? (second ? pb2[i] : pb1[i]) + delta : 0x80000000u;
+            rx[i] = __builtin_amdgcn_raw_buffer_load_b128(second ? x2r : xr, off, 0, 0);
+        }
+    };
+    auto store_regs = [&](int buf) {
+        uint8_t *st = lds + buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) *(u4 *)(st + (NW * wid + i) * 1024 + lane * 16) = rw[i];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) *(u4 *)(st + CT * RB + (NI * wid + i) * 1024 + lane * 16) = rx[i];
+    };
+    load_regs(k0);
+    store_regs(0);
+    if (k0 + 1 < k1) load_regs(k0 + 1);
+    for (int s = k0; s < k1; ++s) {
+        const int buf = (s - k0) & 1;
+        __syncthreads();                              // stage buf written by every wave; step s-1's reads done
+        compute_kc(lds + buf * STAGE, 0);
+        if (s + 1 < k1) {
+            store_regs(buf ^ 1);                      // step s + 1's operands (loaded a step ago)
+            if (s + 2 < k1) load_regs(s + 2);
+        }
+        compute_kc(lds + buf * STAGE, 1);
+    }
+#elif PVC_XRING3
     (void)compute_kc;
     (void)issue;
     issue_x(k0, 0);
