@@ -1139,7 +1139,10 @@ __global__ __launch_bounds__(64 * kNW) void k_conv3x3(ConvArgs a) {
         // issued after weights(s), may still be in flight
         if (s + 1 < k1) __builtin_amdgcn_s_waitcnt(0x0F70 | NI);
         else __builtin_amdgcn_s_waitcnt(0x0F70);
-        __syncthreads();                              // ... every wave's; step s-1's reads are done
+        // ... every wave's; step s-1's reads are done.  A bare s_barrier:
+        // __syncthreads' workgroup release fence would wait for every
+        // outstanding LDS-DMA (vmcnt(0)), pixels(s + 1) included
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         const uint8_t *wst = lds + wb * WST, *xst = lds + 2 * WST + xb * XST;
         compute_kx(wst, xst, 0);
         if (s + 1 < k1) issue_w(s + 1, wb ^ 1);
