@@ -1666,6 +1666,24 @@ constexpr int kMB = 16;                        // pixels per MFMA batch (32 rows
 #ifndef PVM_QUEUE
 #define PVM_QUEUE 128
 #endif
+#ifndef PVM_DMAX
+// 1: the hot-loop band's reference-error term against the sub-chunk box's
+// farthest pixel instead of B (6 % fewer flagged MFMAs on S(1234), but the
+// stream measured 2 % slower: profiles/r06/vote_band_ab.txt)
+#define PVM_DMAX 0
+#endif
+#ifndef PVM_BANDV
+#define PVM_BANDV 2     // band re-check: 2 one FMA a pair to find candidates (round 6), 1 the full per-pair bound (round 5)
+#endif
+#if PVM_DMAX && PVM_BANDV >= 2
+#error "PVM_BANDV 2 derives G from the hot-loop bound, which PVM_DMAX changes"
+#endif
+#ifndef PVM_HOTPRIO
+#define PVM_HOTPRIO 3   // k_vote_mfma's hot-loop issue priority (the rest of the kernel runs at 3)
+#endif
+#ifndef PVM_BANDK
+#define PVM_BANDK 1     // flagged MFMAs re-checked this many at a time (2 measured the same as 1)
+#endif
 // pixels per sub-chunk: a unit's range (~350 px at configs[1]) in one; 352
 // (with a 128-entry band queue) keeps the block's LDS under 40 KiB, so a
 // fourth block -- the next image's -- fits beside a launch's three per CU
@@ -1760,7 +1778,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
     } else {
         even_share(total, nunits, (uint32_t)unit, &lo, &hi);
     }
-    int buf = 0, nfix = 0, nseg = 0, nslow = 0, nxo = 0;
+    int buf = 0, nfix = 0, nseg = 0, nslow = 0, nxo = 0, nqd = 0;   // (nqd: band pairs queued, trace builds)
     uint64_t tloop = 0, t_total = 0, t_hyp = 0;
     uint64_t c_stage = 0, c_hot = 0, c_fix = 0, c_seg = 0, c_mark = 0;   // debug: shader cycles per phase
     uint64_t c_band = 0, c_flush = 0, c_xo = 0;                            // (trace builds: parts of c_fix)
@@ -1946,7 +1964,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                     h4f f = half ? h4f{yl_, yh_, sh, sh} : h4f{xh_, xl_, xh_, yh_};
                     if (!fj) f = h4f{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
                     bf[j] = f;
+#if PVM_DMAX
+                    // the reference-error term against the farthest pixel the
+                    // sub-chunk's box allows, not B: D <= |(|h'x| + axr, |h'y| + ayr)|
+                    // <= |h'| + R (a strip of rows is wide, not tall: 15-30 %
+                    // smaller for hypotheses above or below it)
+                    const float ex = fabsf(hx) + axr, ey = fabsf(hy) + ayr;
+                    const float Dm = __builtin_amdgcn_sqrtf(fmaf(ex, ex, ey * ey)) * 1.0001f;
+                    gb[j] = fj ? (a.gzf * Bv + a.gzr * Dm) * s * 1.00001f : -1.f;
+#else
                     gb[j] = fj ? (a.gzf + a.gzr) * Bv * s * 1.00001f : -1.f;
+#endif
                 }
                 uint32_t neg[kMSet] = {0u, 0u, 0u, 0u};
                 uint64_t hm0 = 0, hm1 = 0;              // band hits: bit 4 p + set, batches 0-15 / 16-31
@@ -1988,6 +2016,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                 const f32x16 zero = {};
                 if (PVV_TRACE_ON(a) && tloop == 0) tloop = __builtin_amdgcn_s_memrealtime();
                 { const uint64_t t = cyc(); c_stage += t - c_mark; c_mark = t; }
+#if PVM_HOTPRIO < 3
+                // the hot loop below the kernel's other phases: a wave in its
+                // prologue, staging or band re-check (latency-bound chains of a
+                // few instructions) issues ahead of the co-resident hot loops
+                __builtin_amdgcn_s_setprio(PVM_HOTPRIO);
+#endif
                 h4f A = afrag(0);
                 f32x16 c0 = __builtin_amdgcn_mfma_f32_32x32x8f16(A, bf[0], zero, 0, 0, 0);
 #pragma unroll 1
@@ -2009,6 +2043,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                     if (p < 16) hm0 |= hbs; else hm1 |= hbs;
                     A = An;
                 }
+#if PVM_HOTPRIO < 3
+                __builtin_amdgcn_s_setprio(3);
+#endif
                 // positives = slots - negatives (padding and never-voting rows are negative)
 #pragma unroll
                 for (int j = 0; j < kMSet; ++j) cnt[j] += ((hfm >> j) & 1u) ? 8 * nb - (int)(neg[j] / 255u) : 0;
@@ -2021,6 +2058,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
 #ifdef PVM_ABL_FIX
                 nfix += __popcll(hm0) + __popcll(hm1);
                 hm0 = hm1 = 0;
+#endif
+#ifdef PVM_ABL_FIX_RT   // the same, decided at run time (the band code stays in the kernel)
+                if (a.rw[3] == 7777) hm0 = hm1 = 0;
 #endif
                 const float kx = a.gzr / tau * 1.0001f, ky = a.gzr * 1.0001f;
                 // the queued pairs by the reference's sequence, one pair per lane;
@@ -2040,6 +2080,88 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                     }
                     nq = 0;
                 };
+#if PVM_BANDV >= 2
+                // Each set's per-pair constant G = gzf B s (1.001), once: from
+                // the hot-loop bound gb = (gzf + gzr) B s (1.00001) with the
+                // same B and s, gb gzf / (gzf + gzr) 1.0011 >= gzf B s 1.001 --
+                // not an hscale (LDS read, sqrt) per flagged MFMA.
+                //
+                // Round 5 tested each pair against g = G + kx |X| + ky |Y|
+                // (~7 VALU a pair, ~90 per flagged MFMA: the band phase was
+                // 12 % of the batch-1 stream, its VALU issued beside three
+                // other waves' hot loops).  Now one FMA a pair decides whether
+                // any pair of the lane can be inside: |Y| <= |X| + |z| for z =
+                // X - |Y| (X >= 0: |Y| = X - z; X < 0: |Y| <= |z|), so |z| <= g
+                // implies |z| (1 - ky) <= G + (kx + ky) |X|, i.e. t = |z| - K |X|
+                // <= G' with K = (kx + ky) / (1 - ky) and G' = G / (1 - ky)
+                // (ky ~ 1e-5; both taken with a 1e-4 margin that also covers
+                // t's rounding).  The pairs with t <= G' are queued for the
+                // reference's sequence: a superset of round 5's queue, so every
+                // decision still equals KU's.
+                float Gs[kMSet];
+                const float gq = a.gzf / (a.gzf + a.gzr) * (1.0011f * 1.0002f);
+#pragma unroll
+                for (int j = 0; j < kMSet; ++j) Gs[j] = gb[j] * gq;
+                const float Kb = (kx + ky) * 1.0002f;
+                auto band_test = [&](const f32x16 &c, int p, int j) {
+                    const bool fj = (hfm >> j) & 1u;
+                    // (selects on the wave-uniform j: a dynamic index would put Gs / bf in scratch)
+                    const float G = j == 0 ? Gs[0] : j == 1 ? Gs[1] : j == 2 ? Gs[2] : Gs[3];
+                    float zs[8], ts[8];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const float X = c[2 * q], Y = c[2 * q + 1];
+                        zs[q] = X - fabsf(Y);
+                        ts[q] = fmaf(-Kb, fabsf(X), fabsf(zs[q]));
+                    }
+                    float mt = __builtin_elementwise_minimum(__builtin_elementwise_minimum(ts[0], ts[1]), ts[2]);
+                    mt = __builtin_elementwise_minimum(__builtin_elementwise_minimum(mt, ts[3]), ts[4]);
+                    mt = __builtin_elementwise_minimum(__builtin_elementwise_minimum(mt, ts[5]), ts[6]);
+                    mt = __builtin_elementwise_minimum(mt, ts[7]);
+                    if (__builtin_amdgcn_ballot_w64(fj && mt <= G)) {
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) {
+                            const int pix = p * kMB + (q & 1) + 4 * (q >> 1) + 2 * half;
+                            const bool u = fj && pix < np && ts[q] <= G;
+                            const uint64_t m = __builtin_amdgcn_ballot_w64(u);
+                            if (m) {
+                                if (nq > kMQueue - kWave) flush();
+                                const int at = nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                                if (u) bq[at] = (uint32_t)pix | ((uint32_t)j << 9) | ((uint32_t)col << 11) | ((signbit(zs[q]) ? 0u : 1u) << 16);
+                                nq += __popcll(m);
+                                nqd += __popcll(m);
+                            }
+                        }
+                    }
+                };
+                static_assert(kMSet == 4, "band selects");
+                auto bsel = [&](int j) -> h4f { return j == 0 ? bf[0] : j == 1 ? bf[1] : j == 2 ? bf[2] : bf[3]; };
+                while (hm0 | hm1) {
+                    int pk[PVM_BANDK], jk[PVM_BANDK], nk = 0;
+#pragma unroll
+                    for (int k = 0; k < PVM_BANDK; ++k) {
+                        pk[k] = 0; jk[k] = 0;
+                        if (hm0 | hm1) {
+                            int bit;
+                            if (hm0) { bit = __builtin_ctzll(hm0); hm0 &= hm0 - 1; }
+                            else { bit = 64 + __builtin_ctzll(hm1); hm1 &= hm1 - 1; }
+                            pk[k] = bit / kMSet; jk[k] = bit % kMSet;
+                            nk = k + 1;
+                        }
+                    }
+                    nfix += nk;
+                    h4f ak[PVM_BANDK];
+#pragma unroll
+                    for (int k = 0; k < PVM_BANDK; ++k) ak[k] = afrag(pk[k]);
+                    f32x16 ck[PVM_BANDK];
+#pragma unroll
+                    for (int k = 0; k < PVM_BANDK; ++k)
+                        ck[k] = __builtin_amdgcn_mfma_f32_32x32x8f16(ak[k], bsel(jk[k]), zero, 0, 0, 0);
+#pragma unroll
+                    for (int k = 0; k < PVM_BANDK; ++k)
+                        if (k < nk) band_test(ck[k], pk[k], jk[k]);
+                }
+#else
                 while (hm0 | hm1) {
                     int bit;
                     if (hm0) { bit = __builtin_ctzll(hm0); hm0 &= hm0 - 1; }
@@ -2082,10 +2204,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                                 const int at = nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
                                 if (u) bq[at] = (uint32_t)pix | ((uint32_t)j << 9) | ((uint32_t)col << 11) | ((signbit(zs[q]) ? 0u : 1u) << 16);
                                 nq += __popcll(m);
+                                nqd += __popcll(m);
                             }
                         }
                     }
                 }
+#endif
                 { const uint64_t t = cyc(); c_band += t - c_mark; c_fix += t - c_mark; c_mark = t; }
                 flush();
                 __builtin_amdgcn_wave_barrier();
@@ -2153,7 +2277,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
         const int wave = (int)(blockIdx.x * 4 + wid);
         uint64_t *q = a.trace + 65536 + wave * 8;
         q[0] = c_seg; q[1] = c_stage; q[2] = c_hot; q[3] = c_fix;
-        q[4] = c_band; q[5] = c_flush; q[6] = c_xo; q[7] = 0;
+        q[4] = c_band; q[5] = c_flush; q[6] = c_xo; q[7] = (uint64_t)nqd;
     }
     if (PVV_TRACE_ON(a) && lane == 0) {
         const int wave = (int)(blockIdx.x * 4 + wid);
@@ -3623,6 +3747,9 @@ void launch_vote(const VoteArgs &va, int64_t pixel_steps, hipStream_t s) {
         VoteArgs vr = va;
         vr.gzf = va.fast ? mfma_gz(va.tau) : 0.f;
         for (int k = 0; k < 4; ++k) vr.rw[k] = 0;
+#ifdef PVM_ABL_FIX_RT
+        vr.rw[3] = 7777;
+#endif
         // a SIMD issues age-first: with one resident block per CU per dispatch
         // round, the rounds' waves end in start order (tools/vote_trace.py:
         // 0 / 3.8 / 7.7 us apart with equal shares); weight the rounds' work

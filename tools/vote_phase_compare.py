@@ -39,7 +39,9 @@ def traced(seg, ver, warm=50):
     nfix = t[:, 3] & 0xffffffff
     names = ["seg", "stage", "hot", "fix", "band", "flush", "xo"]
     tot = c[:, :7].sum(0)
-    return span, dict(zip(names, (tot / len(t)).round(0).tolist())), float(nfix.mean())
+    d = dict(zip(names, (tot / len(t)).round(0).tolist()))
+    d["queued_pairs"] = round(float(c[:, 7].mean()), 2)
+    return span, d, float(nfix.mean())
 
 
 f = synth.synthetic_field(1234)
