@@ -1678,6 +1678,9 @@ constexpr int kMB = 16;                        // pixels per MFMA batch (32 rows
 #if PVM_DMAX && PVM_BANDV >= 2
 #error "PVM_BANDV 2 derives G from the hot-loop bound, which PVM_DMAX changes"
 #endif
+#ifndef PVM_ONEBAR
+#define PVM_ONEBAR 0    // 1: k_vote_mfma<PREPPED> stages a sub-chunk with one barrier (origin = its first / last records' midpoint)
+#endif
 #ifndef PVM_HOTPRIO
 #define PVM_HOTPRIO 3   // k_vote_mfma's hot-loop issue priority (the rest of the kernel runs at 3)
 #endif
@@ -1801,12 +1804,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
         // ---- segment: pixels [ts, te) of (b, v) against hypotheses hg*128 .. +127 ----
         c_mark = cyc();
         F4 L[kMSlots];
+        // (PVM_ONEBAR: the sub-chunk's first and last records, whose midpoint is
+        // the origin -- row-major compacted records: a strip of rows)
+        float fx0 = 0.f, fy0 = 0.f, fx1 = 0.f, fy1 = 0.f;
         auto load_px = [&](int s0, int np) {
 #pragma unroll
             for (int k = 0; k < kMSlots; ++k) {
                 const int t = k * 256 + wid * kWave + lane;
                 L[k] = F4{0.f, 0.f, 0.f, 0.f};
                 if (t < np) L[k] = pixel_exact<PREPPED>(a, b, v, s0 + t);
+            }
+            if (PVM_ONEBAR && PREPPED) {
+                const F4 e0 = pixel_exact<PREPPED>(a, b, v, s0), e1 = pixel_exact<PREPPED>(a, b, v, s0 + np - 1);
+                fx0 = e0.x; fy0 = e0.y; fx1 = e1.x; fy1 = e1.y;
             }
         };
         load_px(ts, min(kMChunk, te - ts));
@@ -1896,6 +1906,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                 QB.box[wid] = make_float4(kBig, -kBig, kBig, -kBig);
                 QB.exo[wid] = 0;
             }
+            // the form rows of the sub-chunk's pixels against origin (ox, oy)
+            auto put_rows = [&](float ox, float oy, bool slow) {
+#pragma unroll
+                for (int k = 0; k < kMSlots; ++k) {
+                    const int tt = k * 256 + t;
+                    if (tt >= kMChunk) break;
+                    uint4 rx = make_uint4(0u, 0u, pack_h2((_Float16)0.f, (_Float16)0.f),
+                                          pack_h2((_Float16)(-60000.f), (_Float16)0.f));   // never votes: X = -6e4 s
+                    uint4 ry = make_uint4(0u, 0u, 0u, 0u);
+                    if (q[k].x == q[k].x && !slow) {
+                        const float cx = q[k].x - ox, cy = q[k].y - oy;      // exact for pixel centres
+                        const float axX = tau * q[k].z, ayX = tau * q[k].w;
+                        rx = form_row(axX, ayX, fmaf(axX, cx, ayX * cy));
+                        ry = form_row(-q[k].w, q[k].z, fmaf(-q[k].w, cx, q[k].z * cy));
+                    }
+                    S.rows[tt >> 4][2 * (tt & 15)] = rx;
+                    S.rows[tt >> 4][2 * (tt & 15) + 1] = ry;
+                }
+            };
+            constexpr bool onebar = PVM_ONEBAR && PREPPED;
+            float ox = 0.f, oy = 0.f;
+            if constexpr (onebar) {
+                // One barrier per sub-chunk: the origin is the midpoint of the
+                // sub-chunk's first and last records (known to every thread
+                // before any reduction), the rows are written against it
+                // before the barrier, and the box reduction after it only
+                // measures R about that origin (an origin anywhere keeps every
+                // decision exact; a central one keeps R, so the band, small)
+                ox = floorf(0.5f * fx0 + 0.5f * fx1);
+                oy = floorf(0.5f * fy0 + 0.5f * fy1);
+                if (!(fabsf(ox) <= 1.6e7f && fabsf(oy) <= 1.6e7f)) { ox = 0.f; oy = 0.f; }
+                ox = __builtin_amdgcn_readfirstlane(ox);
+                oy = __builtin_amdgcn_readfirstlane(oy);
+                put_rows(ox, oy, !a.fast);
+            }
             // next sub-chunk's loads, in flight across the barriers and the hot loop
             if (s0 + kMChunk < te) load_px(s0 + kMChunk, min(kMChunk, te - s0 - kMChunk));
             __syncthreads();
@@ -1908,31 +1953,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                 cyl = fminf(cyl, Q.z); cyh = fmaxf(cyh, Q.w);
                 exq |= QB.exo[k];
             }
-            float ox = floorf(0.5f * cxl + 0.5f * cxh), oy = floorf(0.5f * cyl + 0.5f * cyh);
-            if (!(fabsf(ox) <= 1.6e7f && fabsf(oy) <= 1.6e7f)) { ox = 0.f; oy = 0.f; }
+            if constexpr (!onebar) {
+                ox = floorf(0.5f * cxl + 0.5f * cxh), oy = floorf(0.5f * cyl + 0.5f * cyh);
+                if (!(fabsf(ox) <= 1.6e7f && fabsf(oy) <= 1.6e7f)) { ox = 0.f; oy = 0.f; }
+            }
             const float axr = fmaxf(cxh - ox, ox - cxl), ayr = fmaxf(cyh - oy, oy - cyl);
             const float R = __builtin_amdgcn_sqrtf(fmaf(axr, axr, ayr * ayr)) * 1.00001f;
             // (the fp16 b operands reach max(tau, 1) R: tau u.c' for X, u x c' for Y)
             bool slow = !a.fast || exq != 0 || !(R * fmaxf(tau, 1.f) <= kMRMax);
             slow = __builtin_amdgcn_readfirstlane(slow);
             nslow += slow ? 1 : 0;
-#pragma unroll
-            for (int k = 0; k < kMSlots; ++k) {
-                const int tt = k * 256 + t;
-                if (tt >= kMChunk) break;
-                uint4 rx = make_uint4(0u, 0u, pack_h2((_Float16)0.f, (_Float16)0.f),
-                                      pack_h2((_Float16)(-60000.f), (_Float16)0.f));   // never votes: X = -6e4 s
-                uint4 ry = make_uint4(0u, 0u, 0u, 0u);
-                if (q[k].x == q[k].x && !slow) {
-                    const float cx = q[k].x - ox, cy = q[k].y - oy;      // exact for pixel centres
-                    const float axX = tau * q[k].z, ayX = tau * q[k].w;
-                    rx = form_row(axX, ayX, fmaf(axX, cx, ayX * cy));
-                    ry = form_row(-q[k].w, q[k].z, fmaf(-q[k].w, cx, q[k].z * cy));
-                }
-                S.rows[tt >> 4][2 * (tt & 15)] = rx;
-                S.rows[tt >> 4][2 * (tt & 15) + 1] = ry;
+            if constexpr (!onebar) {
+                put_rows(ox, oy, slow);
+                __syncthreads();
             }
-            __syncthreads();
             if (!slow) {
                 // ---- the hypotheses' B fragments and bands for this origin ----
                 // hypothesis j's scale s = 2^-k (|h' s| < 2^14) and bound B >=
