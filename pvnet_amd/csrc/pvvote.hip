@@ -2128,15 +2128,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                 // X - |Y| (X >= 0: |Y| = X - z; X < 0: |Y| <= |z|), so |z| <= g
                 // implies |z| (1 - ky) <= G + (kx + ky) |X|, i.e. t = |z| - K |X|
                 // <= G' with K = (kx + ky) / (1 - ky) and G' = G / (1 - ky)
-                // (ky ~ 1e-5; both taken with a 1e-4 margin that also covers
-                // t's rounding).  The pairs with t <= G' are queued for the
+                // (both with a 2e-4 margin that also covers t's rounding;
+                // tests/test_band_filter.py checks the inclusion in float32).  The pairs with t <= G' are queued for the
                 // reference's sequence: a superset of round 5's queue, so every
                 // decision still equals KU's.
+                // (1 / (1 - ky): ky reaches 8e-4 at thr 0.999999 -- gzr grows with 1/tau)
+                const float inv1k = 1.0002f / (1.f - ky * 1.0001f);
                 float Gs[kMSet];
-                const float gq = a.gzf / (a.gzf + a.gzr) * (1.0011f * 1.0002f);
+                const float gq = a.gzf / (a.gzf + a.gzr) * 1.0011f * inv1k;
 #pragma unroll
                 for (int j = 0; j < kMSet; ++j) Gs[j] = gb[j] * gq;
-                const float Kb = (kx + ky) * 1.0002f;
+                const float Kb = (kx + ky) * inv1k;
                 auto band_test = [&](const f32x16 &c, int p, int j) {
                     const bool fj = (hfm >> j) & 1u;
                     // (selects on the wave-uniform j: a dynamic index would put Gs / bf in scratch)
