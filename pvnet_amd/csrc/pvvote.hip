@@ -4003,7 +4003,7 @@ const char *pv_version(void) { return PV_VERSION; }
 #define PVV_STR2(x) #x
 #define PVV_STR(x) PVV_STR2(x)
 const char *pv_build_config(void) {
-    return "vote=k_vote_mfma(bpc=" PVV_STR(PVV_VM_BPC) ",wpe=" PVM_WPE_STR ",chunk=" PVV_STR(PVM_CHUNK) ",queue=" PVV_STR(PVM_QUEUE) ",rw=" PVV_STR(PVV_VM_RW3_0) "/"
+    return "vote=k_vote_mfma(bpc=" PVV_STR(PVV_VM_BPC) ",wpe=" PVM_WPE_STR ",chunk=" PVV_STR(PVM_CHUNK) ",queue=" PVV_STR(PVM_QUEUE) ",band=" PVV_STR(PVM_BANDV) ",rw=" PVV_STR(PVV_VM_RW3_0) "/"
            PVV_STR(PVV_VM_RW3_1) "/" PVV_STR(PVV_VM_RW3_2) ")"
            " hypgen=" PVV_STR(PVV_HYPGEN) " hypfuse=" PVV_STR(PVV_HYPFUSE)
            " refine=" PVV_STR(PVV_REFINE_NJ) "x" PVV_STR(PVV_REFINE_T)
