@@ -292,6 +292,19 @@ __device__ __forceinline__ int wave_sum_i(int x) {
     const auto r32 = __builtin_amdgcn_permlane32_swap(x, x, false, false);
     return (int)(r32[0] + r32[1]);
 }
+// inclusive prefix sum over the wave by DPP: row_shr 1/2/4/8 within each
+// 16-lane row (bound_ctrl: lanes past the row start add 0), then row_bcast15
+// (rows 1, 3) and row_bcast31 (rows 2, 3) -- no ds_bpermute round trips
+// (the __shfl_up form is six serial LDS latencies)
+__device__ __forceinline__ int wave_incl_scan_i(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);
+    return x;
+}
 __device__ __forceinline__ double wave_sum_d(double x) {
     for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
     return x;
@@ -649,6 +662,9 @@ __device__ __forceinline__ void compact_chunk(const VertexView &vx, int H, int W
 // ballots), one kernel fewer in the call's chain: a k_hyp_gen launch costs
 // the batch-1 stream ~9 % (profiles/r06/ablation.txt).
 // ==========================================================================
+#ifndef PVV_HYP_FASTSEARCH
+#define PVV_HYP_FASTSEARCH 0   // 1: compact_hyp with a DPP wave scan and an 8-ary chunk search (bit-identical; measured neutral)
+#endif
 constexpr int kHypMaxChunks = 1536;   // chunks per image the fused hypotheses handle (LDS prefix); more: k_hyp_gen
 struct HypGen {
     int nhb;                    // hypothesis blocks per image (0: none, k_hyp_gen runs)
@@ -716,12 +732,16 @@ __device__ void compact_hyp(const VertexView &vx, int H, int W, int nblk, const 
 #pragma unroll
         for (int k = 0; k < 6; ++k) run += v[k];
         // inclusive wave scan of run (row shifts + row broadcasts)
+#if PVV_HYP_FASTSEARCH
+        const int x = wave_incl_scan_i(run);
+#else
         int x = run;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const int y = __shfl_up(x, o);
             if (lane_id() >= o) x += y;
         }
+#endif
         __syncthreads();
         if (lane_id() == 63) sh[threadIdx.x / 64] = x;
         __syncthreads();
@@ -801,6 +821,27 @@ __device__ void compact_hyp(const VertexView &vx, int H, int W, int nblk, const 
 #pragma unroll
     for (int e = 0; e < 2; ++e) {                  // the last chunk with pre <= t (never an empty one)
         int lo = 0, hi = nblk - 1;
+#if PVV_HYP_FASTSEARCH
+        // 8-ary: seven pivots read together per step (4 dependent LDS trips
+        // for 1,200 chunks instead of 11); the same index as the bisection
+        while (hi - lo >= 8) {
+            int pv[7], cnt = 0;
+#pragma unroll
+            for (int k = 0; k < 7; ++k) pv[k] = lo + (int)(((int64_t)(hi - lo) * (k + 1) + 7) / 8);
+            int vv[7];
+#pragma unroll
+            for (int k = 0; k < 7; ++k) vv[k] = pre[pv[k]];
+#pragma unroll
+            for (int k = 0; k < 7; ++k) cnt += vv[k] <= t[e] ? 1 : 0;
+            int nlo = lo, nhi = hi;
+#pragma unroll
+            for (int k = 0; k < 7; ++k) {
+                if (cnt == k + 1) nlo = pv[k];
+                if (cnt == k) nhi = pv[k] - 1;
+            }
+            lo = nlo; hi = nhi;
+        }
+#endif
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
             if (pre[mid] <= t[e]) lo = mid; else hi = mid - 1;
