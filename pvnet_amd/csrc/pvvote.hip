@@ -2195,6 +2195,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PVM_WPE, PV
                     mt = __builtin_elementwise_minimum(__builtin_elementwise_minimum(mt, ts[3]), ts[4]);
                     mt = __builtin_elementwise_minimum(__builtin_elementwise_minimum(mt, ts[5]), ts[6]);
                     mt = __builtin_elementwise_minimum(mt, ts[7]);
+#ifdef PVM_ABL_Q_RT   // profiling: the candidates found but never queued (counts wrong)
+                    if (a.rw[3] == 7778) mt = 3.0e38f;
+#endif
                     if (__builtin_amdgcn_ballot_w64(fj && mt <= G)) {
 #pragma unroll
                         for (int q = 0; q < 8; ++q) {
@@ -3826,6 +3829,9 @@ void launch_vote(const VoteArgs &va, int64_t pixel_steps, hipStream_t s) {
         for (int k = 0; k < 4; ++k) vr.rw[k] = 0;
 #ifdef PVM_ABL_FIX_RT
         vr.rw[3] = 7777;
+#endif
+#ifdef PVM_ABL_Q_RT
+        vr.rw[3] = 7778;
 #endif
         // a SIMD issues age-first: with one resident block per CU per dispatch
         // round, the rounds' waves end in start order (tools/vote_trace.py:
